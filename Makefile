@@ -1,0 +1,21 @@
+# Build for MI355X (gfx950). No cmake: plain hipcc / gcc.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Wno-unused-result
+LIB = meyda_amd/libmeyda_gpu.so
+SRC = meyda_amd/csrc/kernels.hip meyda_amd/csrc/plan.cpp
+HDR = include/meyda_gpu.h meyda_amd/csrc/mgx_internal.h
+
+all: $(LIB) oracle
+
+$(LIB): $(SRC) $(HDR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ -x hip $(SRC)
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -f $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Benchmark of the meyda hot path on MI355X.
+
+Metric (BASELINE.json): audio frames/sec at bufferSize=1024 with all features, on
+1/2/4/8 GPUs, and the fraction of the HBM roofline.
+
+A "step" is one fused extraction launch over one batch of 262,144 synthetic frames
+of 1024 float32 samples per GPU (BASELINE config C3/C4 size), computing every
+per-frame feature: rms, energy, zcr, spectralCentroid/Flatness/Slope/Rolloff/
+Spread/Skewness/Kurtosis, loudness (24 specific + total), perceptualSpread,
+perceptualSharpness, mfcc (13). Inputs are generated in HBM before the timed
+region. Multi-GPU: one process per GPU (torch.distributed), each rank extracts
+its own 262,144-frame shard (weak scaling, no data-path collective); rank 0
+prints the JSON line with the whole-job frames/s (max elapsed over ranks).
+"""
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from meyda_amd import capi  # noqa: E402
+
+FEATURES = capi.ALL_FEATURES  # 13 scalars + loudness.specific(24) + mfcc(13)
+OUT_FLOATS = 3 + 7 + 25 + 2 + 13  # per frame, f32 outputs
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--frames", type=int, default=262144, help="frames per GPU per step")
+    ap.add_argument("--precision", default="faithful", choices=["faithful", "fast"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--also-fast", action="store_true", help="report the fp32 mode alongside")
+    return ap.parse_args()
+
+
+def cpu_baseline(n, seconds):
+    """Time the CPU oracle (C restatement of the reference path) on host cores."""
+    from oracle import oracle
+    oracle.lib()
+    threads = min(16, os.cpu_count() or 1)
+    per = 256
+    x = oracle.synth_frames(capi_seed(), 0, per * threads, n)
+
+    def work(i):
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            oracle.extract(x[i * per:(i + 1) * per])
+            done += per
+        return done, time.perf_counter() - t0
+
+    with cf.ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        res = list(ex.map(work, range(threads)))
+        wall = time.perf_counter() - t0
+    frames = sum(r[0] for r in res)
+    one = work(0)
+    return {"value": frames / wall, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": "%d frames (N=%d, all features, seeded noise) over %.1f s on %d threads; "
+                      "1 thread: %.0f frames/s" % (frames, n, wall, threads, one[0] / one[1])}
+
+
+def capi_seed():
+    import meyda_amd
+    return meyda_amd.SEED
+
+
+def run_mode(plan, frames, out, steps, warmup, dist, world):
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup):
+        plan.extract_device(frames.data_ptr(), frames.shape[0], out, stream.cuda_stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        plan.extract_device(frames.data_ptr(), frames.shape[0], out, stream.cuda_stream)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, kernel_ms
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+    else:
+        torch.cuda.set_device(0)
+    n, F = args.n, args.frames
+    frames = torch.empty(F, n, dtype=torch.float32, device="cuda")
+    # each rank its own shard of one global synthetic stream
+    capi.synth_frames_device(frames, capi_seed(), first_frame=rank * F)
+    plan = capi.Plan(buffer_size=n, precision=args.precision, device=torch.cuda.current_device())
+    outs, o = plan.alloc_outputs(F, FEATURES)
+    torch.cuda.synchronize()
+    elapsed, kernel_ms = run_mode(plan, frames, o, args.steps, args.warmup, dist, world)
+    fast = None
+    if args.also_fast and args.precision != "fast":
+        plan_f = capi.Plan(buffer_size=n, precision="fast", device=torch.cuda.current_device())
+        el_f, km_f = run_mode(plan_f, frames, o, args.steps, args.warmup, dist, world)
+        fast = {"value": world * F * args.steps / el_f, "kernel_ms": km_f,
+                "roofline_frac": (F * (4 * n + 4 * OUT_FLOATS)) / (km_f * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    if rank == 0:
+        bytes_per_frame = 4 * n + 4 * OUT_FLOATS
+        achieved = F * bytes_per_frame / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(prof):
+            with open(prof) as fh:
+                pj = json.load(fh)
+            key = "%s_n%d_f%d" % (args.precision, n, F)
+            if key in pj:
+                traffic = pj[key]["hbm_bytes_per_launch"]
+        line = {
+            "metric": "audio frames/sec (bufferSize=1024, all features) at 1/2/4/8 GPUs; % HBM roofline",
+            "value": world * F * args.steps / elapsed,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64 butterflies / f32 storage" if args.precision == "faithful" else "f32",
+            "data": "synthetic (seeded splitmix64 PCM generated in HBM)",
+            "config": {"workload": "C3+C4 all features: %d frames x bufferSize=%d per GPU, float32 outputs" % (F, n),
+                       "buffer_size": n, "frames_per_gpu": F, "features": FEATURES,
+                       "precision": args.precision, "parallelism": "frame shards, %d proc" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
+                         "bytes_per_frame": bytes_per_frame},
+        }
+        if fast:
+            line["fast_mode"] = fast
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,172 @@
+/*
+ * meyda_gpu.h — C ABI of the MI355X (gfx950) meyda feature-extraction engine.
+ *
+ * This is the drop-in boundary for the reference's per-buffer hot path. In the
+ * reference (kirbysayshi/meyda), one call of the path is:
+ *
+ *   src/meyda.js:69-91    onaudioprocess: window -> (FFT) -> amplitude spectrum
+ *   src/meyda.js:244-261  Meyda.get(feature | features[]) -> extractor modules
+ *   src/extractors/NAME.js  the 18 extractor plugins, signature (bufferSize, m)
+ *
+ * The engine batches that path: many frames of `buffer_size` Float32 samples are
+ * processed by one fused HIP launch. A host binding (the N-API addon under
+ * meyda_amd/addon/, or ctypes) maps Meyda's get()/start()/stop() onto it.
+ *
+ * Entry points and the reference interface each one replaces:
+ *   mgx_plan_create      new Meyda(audioContext, src, bufferSize)   src/meyda.js:17-97
+ *                        (power-of-two check src/meyda.js:20-22, tables :44-48,
+ *                         extractor init :208-225)
+ *   mgx_extract_device   onaudioprocess + get(features)             src/meyda.js:69-91,244-261
+ *   mgx_extract_host     same, for host (pageable) buffers
+ *   mgx_feature_index    the extractor registry by name             src/extractors/index.js:1-20
+ *   mgx_feature_info     featureInfo[name].type                     src/feature-info.js:1-65
+ *   mgx_last_error       console.error / thrown Error text          src/meyda.js:20-26,249-253
+ *
+ * Conventions: every function returns an int status (MGX_OK = 0, negative =
+ * MGX_E_*); the message of the last failure on the calling thread is returned
+ * by mgx_last_error(). Plans are not thread-safe; distinct plans are
+ * independent. No torch or HIP types appear in these signatures: streams are
+ * passed as `void*` (a hipStream_t, or NULL for the default stream).
+ */
+#ifndef MEYDA_GPU_H
+#define MEYDA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGX_ABI_VERSION 1
+
+typedef enum mgx_status {
+  MGX_OK = 0,
+  MGX_E_INVALID_ARGUMENT = -1,   /* NULL pointer, bad enum, bad struct_size */
+  MGX_E_NOT_POWER_OF_TWO = -2,   /* "Buffer size is not a power of two" (src/meyda.js:20-22) */
+  MGX_E_UNSUPPORTED = -3,        /* valid request this build does not implement */
+  MGX_E_DEVICE = -4,             /* a HIP runtime call failed */
+  MGX_E_OUT_OF_MEMORY = -5,
+  MGX_E_NO_DEVICE = -6           /* no usable gfx950 device */
+} mgx_status;
+
+/* Feature indices. The first 13 are the per-frame scalar record, in this order. */
+typedef enum mgx_feature {
+  MGX_RMS = 0,                  /* src/extractors/rms.js */
+  MGX_ENERGY = 1,               /* energy.js */
+  MGX_ZCR = 2,                  /* zcr.js (exact integer count) */
+  MGX_SPECTRAL_CENTROID = 3,    /* spectralCentroid.js (bin units, as the reference) */
+  MGX_SPECTRAL_FLATNESS = 4,    /* spectralFlatness.js */
+  MGX_SPECTRAL_SLOPE = 5,       /* spectralSlope.js */
+  MGX_SPECTRAL_ROLLOFF = 6,     /* spectralRolloff.js (Hz) */
+  MGX_SPECTRAL_SPREAD = 7,      /* spectralSpread.js */
+  MGX_SPECTRAL_SKEWNESS = 8,    /* spectralSkewness.js */
+  MGX_SPECTRAL_KURTOSIS = 9,    /* spectralKurtosis.js */
+  MGX_LOUDNESS_TOTAL = 10,      /* loudness.js .total */
+  MGX_PERCEPTUAL_SPREAD = 11,   /* perceptualSpread.js */
+  MGX_PERCEPTUAL_SHARPNESS = 12,/* perceptualSharpness.js */
+  MGX_NUM_SCALARS = 13,
+  /* vector features (pointer fields of mgx_outputs) */
+  MGX_LOUDNESS = 13,            /* loudness.js: {specific: Float32Array(24), total} */
+  MGX_MFCC = 14,                /* mfcc.js: Float32Array(13) */
+  MGX_AMPLITUDE_SPECTRUM = 15,  /* amplitudeSpectrum.js */
+  MGX_POWER_SPECTRUM = 16,      /* powerSpectrum.js */
+  MGX_COMPLEX_SPECTRUM = 17,    /* complexSpectrum.js: {real, imag} */
+  MGX_BUFFER = 18,              /* buffer (declared in feature-info.js:3-5): the frame itself */
+  MGX_NUM_FEATURES = 19
+} mgx_feature;
+
+typedef enum mgx_window { MGX_WINDOW_HANNING = 0, MGX_WINDOW_HAMMING = 1 } mgx_window;
+
+typedef enum mgx_precision {
+  /* FP64 butterflies, every radix-2 stage rounded to float32 as jsfft stores it
+   * (lib/jsfft/fft.js:153-161 + Float32Array storage). Parity default. */
+  MGX_PRECISION_FAITHFUL = 0,
+  /* float32 butterflies: HBM-bound, matches the reference only on broadband input. */
+  MGX_PRECISION_FAST = 1
+} mgx_precision;
+
+typedef enum mgx_mode {
+  MGX_MODE_PER_BUFFER_FFT = 0,  /* the intended path: FFT of every buffer */
+  MGX_MODE_LITERAL = 1          /* the snapshot's behaviour: ampSpectrum = |window * x|,
+                                   no per-buffer FFT (src/meyda.js:79-84,184-197) */
+} mgx_mode;
+
+typedef enum mgx_info_type { MGX_TYPE_NUMBER = 0, MGX_TYPE_ARRAY = 1, MGX_TYPE_MULTIPLE_ARRAYS = 2 } mgx_info_type;
+
+typedef struct mgx_plan_desc {
+  uint32_t struct_size;      /* = sizeof(mgx_plan_desc) */
+  uint32_t buffer_size;      /* N: power of two; the GPU path supports 256 <= N <= 2048 */
+  double sample_rate;        /* audioContext.sampleRate */
+  uint32_t window;           /* mgx_window (Meyda.windowingFunction) */
+  uint32_t precision;        /* mgx_precision */
+  uint32_t mode;             /* mgx_mode */
+  uint32_t num_bark_bands;   /* 24 (loudness.js NUM_BARK_BANDS) */
+  uint32_t num_mel_bands;    /* 26 in the reference (mfcc.js:15); 1..64 supported */
+  uint32_t num_mfcc_coeffs;  /* 13 (mfcc.js:71) */
+  uint32_t scalar_f64;       /* 0: scalar outputs are float32 arrays, 1: float64 */
+  int32_t device;            /* HIP device ordinal */
+} mgx_plan_desc;
+
+typedef struct mgx_plan mgx_plan;
+
+/* Output arrays, structure of arrays over frames. Any pointer may be NULL: the
+ * corresponding feature is then not written (and, where possible, not computed).
+ * scalars[i] points to num_frames floats (or doubles if scalar_f64). */
+typedef struct mgx_outputs {
+  void* scalars[MGX_NUM_SCALARS];
+  float* loudness_specific;   /* num_frames x num_bark_bands */
+  float* mfcc;                /* num_frames x num_mfcc_coeffs */
+  float* amplitude_spectrum;  /* num_frames x N/2 */
+  float* power_spectrum;      /* num_frames x N/2 */
+  float* complex_real;        /* num_frames x N */
+  float* complex_imag;        /* num_frames x N */
+} mgx_outputs;
+
+/* Host-side tables of a plan (no device needed): used by tests and by bindings
+ * that want to show the same tables Meyda exposes (hanning, hamming, barkScale). */
+typedef struct mgx_host_tables {
+  float* window;        /* N */
+  float* hanning;       /* N */
+  float* hamming;       /* N */
+  float* bark_scale;    /* N */
+  int32_t* bark_limits; /* num_bark_bands + 1 */
+  int32_t* mel_bins;    /* num_mel_bands + 2 */
+  float* dct;           /* num_mfcc_coeffs * num_mel_bands, layout dct[c + j*num_mfcc_coeffs] */
+} mgx_host_tables;
+
+void mgx_plan_desc_init(mgx_plan_desc* desc);
+int mgx_plan_create(const mgx_plan_desc* desc, mgx_plan** out_plan);
+int mgx_plan_destroy(mgx_plan* plan);
+int mgx_plan_get_desc(const mgx_plan* plan, mgx_plan_desc* out_desc);
+
+/* Device-resident batch: frames and every non-NULL output are device pointers.
+ * Asynchronous on `stream` (hipStream_t or NULL). */
+int mgx_extract_device(mgx_plan* plan, const float* frames, uint64_t num_frames,
+                       const mgx_outputs* outputs, void* stream);
+
+/* Host batch: frames and outputs in host memory; stages through plan-owned
+ * device buffers in chunks and returns when the outputs are written. */
+int mgx_extract_host(mgx_plan* plan, const float* frames, uint64_t num_frames,
+                     const mgx_outputs* outputs);
+
+/* Synthetic PCM written straight into HBM:
+ * x[i] = (splitmix64(seed + (i+1)*0x9E3779B97F4A7C15) >> 40) * 2^-23 - 1,
+ * i = first_frame*N + t for t < num_frames*N. */
+int mgx_synth_frames_device(float* frames, uint64_t num_frames, uint32_t buffer_size,
+                            uint64_t seed, uint64_t first_frame, void* stream);
+
+int mgx_get_host_tables(const mgx_plan_desc* desc, const mgx_host_tables* out);
+
+int mgx_is_power_of_two(double n);           /* src/utils.js:13-19 */
+int mgx_feature_index(const char* name);     /* -1 if unknown */
+const char* mgx_feature_name(int feature);   /* NULL if out of range */
+int mgx_feature_info(int feature);           /* mgx_info_type, or -1 */
+int mgx_device_count(int* count);
+int mgx_abi_version(void);
+const char* mgx_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MEYDA_GPU_H */

@@ -1,0 +1,270 @@
+"""ctypes binding of the C ABI in include/meyda_gpu.h (libmeyda_gpu.so, built in-tree).
+
+This is plumbing for the Python test suite and bench.py; the product host binding
+for the reference's JavaScript API is the N-API addon (meyda_amd/addon/) used by
+meyda_amd/js/meyda.js. There is no CPU fallback here: if the HIP library is
+missing or no gfx950 device is present, every compute call raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmeyda_gpu.so")
+
+NUM_SCALARS = 13
+NUM_BARK = 24
+SCALAR_NAMES = ["rms", "energy", "zcr", "spectralCentroid", "spectralFlatness", "spectralSlope",
+                "spectralRolloff", "spectralSpread", "spectralSkewness", "spectralKurtosis",
+                "loudness.total", "perceptualSpread", "perceptualSharpness"]
+FEATURE_NAMES = SCALAR_NAMES + ["loudness", "mfcc", "amplitudeSpectrum", "powerSpectrum",
+                                "complexSpectrum", "buffer"]
+WINDOWS = {"hanning": 0, "hamming": 1}
+PRECISIONS = {"faithful": 0, "fast": 1}
+MODES = {"per_buffer_fft": 0, "literal": 1}
+
+STATUS = {0: "MGX_OK", -1: "MGX_E_INVALID_ARGUMENT", -2: "MGX_E_NOT_POWER_OF_TWO",
+          -3: "MGX_E_UNSUPPORTED", -4: "MGX_E_DEVICE", -5: "MGX_E_OUT_OF_MEMORY",
+          -6: "MGX_E_NO_DEVICE"}
+
+# Every symbol include/meyda_gpu.h declares (checked by tests/test_capi_host.py).
+EXPORTS = ["mgx_plan_desc_init", "mgx_plan_create", "mgx_plan_destroy", "mgx_plan_get_desc",
+           "mgx_extract_device", "mgx_extract_host", "mgx_synth_frames_device",
+           "mgx_get_host_tables", "mgx_is_power_of_two", "mgx_feature_index", "mgx_feature_name",
+           "mgx_feature_info", "mgx_device_count", "mgx_abi_version", "mgx_last_error"]
+
+
+class MgxError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__("%s (%d): %s" % (STATUS.get(status, "?"), status, message))
+        self.status = status
+
+
+class PlanDesc(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("buffer_size", ctypes.c_uint32),
+                ("sample_rate", ctypes.c_double), ("window", ctypes.c_uint32),
+                ("precision", ctypes.c_uint32), ("mode", ctypes.c_uint32),
+                ("num_bark_bands", ctypes.c_uint32), ("num_mel_bands", ctypes.c_uint32),
+                ("num_mfcc_coeffs", ctypes.c_uint32), ("scalar_f64", ctypes.c_uint32),
+                ("device", ctypes.c_int32)]
+
+
+class Outputs(ctypes.Structure):
+    _fields_ = [("scalars", ctypes.c_void_p * NUM_SCALARS),
+                ("loudness_specific", ctypes.c_void_p), ("mfcc", ctypes.c_void_p),
+                ("amplitude_spectrum", ctypes.c_void_p), ("power_spectrum", ctypes.c_void_p),
+                ("complex_real", ctypes.c_void_p), ("complex_imag", ctypes.c_void_p)]
+
+
+class HostTables(ctypes.Structure):
+    _fields_ = [("window", ctypes.c_void_p), ("hanning", ctypes.c_void_p),
+                ("hamming", ctypes.c_void_p), ("bark_scale", ctypes.c_void_p),
+                ("bark_limits", ctypes.c_void_p), ("mel_bins", ctypes.c_void_p),
+                ("dct", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libmeyda_gpu.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libmeyda_gpu.so not built (run `make` or __graft_entry__.build())")
+        # torch ships its own libamdhip64 (SONAME libamdhip64.so.7). Load it first so
+        # the loader resolves our DT_NEEDED libamdhip64.so.7 to that same runtime:
+        # two HIP runtimes in one process leave the second without devices.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = ctypes.CDLL(LIB_PATH)
+        L.mgx_plan_desc_init.argtypes = [ctypes.POINTER(PlanDesc)]
+        L.mgx_plan_desc_init.restype = None
+        L.mgx_plan_create.argtypes = [ctypes.POINTER(PlanDesc), ctypes.POINTER(ctypes.c_void_p)]
+        L.mgx_plan_destroy.argtypes = [ctypes.c_void_p]
+        L.mgx_plan_get_desc.argtypes = [ctypes.c_void_p, ctypes.POINTER(PlanDesc)]
+        L.mgx_extract_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                         ctypes.POINTER(Outputs), ctypes.c_void_p]
+        L.mgx_extract_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                       ctypes.POINTER(Outputs)]
+        L.mgx_synth_frames_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                              ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+        L.mgx_get_host_tables.argtypes = [ctypes.POINTER(PlanDesc), ctypes.POINTER(HostTables)]
+        L.mgx_is_power_of_two.argtypes = [ctypes.c_double]
+        L.mgx_feature_index.argtypes = [ctypes.c_char_p]
+        L.mgx_feature_name.argtypes = [ctypes.c_int]
+        L.mgx_feature_name.restype = ctypes.c_char_p
+        L.mgx_feature_info.argtypes = [ctypes.c_int]
+        L.mgx_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.mgx_last_error.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise MgxError(rc, lib().mgx_last_error().decode())
+    return rc
+
+
+def make_desc(buffer_size=512, sample_rate=44100.0, window="hanning", precision="faithful",
+              mode="per_buffer_fft", num_mel_bands=26, num_mfcc_coeffs=13, scalar_f64=False,
+              device=0):
+    d = PlanDesc()
+    lib().mgx_plan_desc_init(ctypes.byref(d))
+    d.buffer_size = buffer_size
+    d.sample_rate = sample_rate
+    d.window = WINDOWS[window]
+    d.precision = PRECISIONS[precision]
+    d.mode = MODES[mode]
+    d.num_mel_bands = num_mel_bands
+    d.num_mfcc_coeffs = num_mfcc_coeffs
+    d.scalar_f64 = 1 if scalar_f64 else 0
+    d.device = device
+    return d
+
+
+def host_tables(**kw):
+    """Host tables (window, bark, limits, mel bins, dct) computed by the library: no GPU."""
+    d = make_desc(**kw)
+    n, nf, nc = d.buffer_size, d.num_mel_bands, d.num_mfcc_coeffs
+    t = {"window": np.empty(n, np.float32), "hanning": np.empty(n, np.float32),
+         "hamming": np.empty(n, np.float32), "bark_scale": np.empty(n, np.float32),
+         "bark_limits": np.empty(NUM_BARK + 1, np.int32), "mel_bins": np.empty(nf + 2, np.int32),
+         "dct": np.empty(nc * nf, np.float32)}
+    ht = HostTables(*[t[k].ctypes.data for k in ("window", "hanning", "hamming", "bark_scale",
+                                                  "bark_limits", "mel_bins", "dct")])
+    check(lib().mgx_get_host_tables(ctypes.byref(d), ctypes.byref(ht)))
+    return t
+
+
+def device_count():
+    c = ctypes.c_int(0)
+    check(lib().mgx_device_count(ctypes.byref(c)))
+    return c.value
+
+
+class Plan:
+    """One extraction plan (mirrors `new Meyda(ctx, src, bufferSize)`, src/meyda.js:17-97)."""
+
+    def __init__(self, buffer_size=512, **kw):
+        self.desc = make_desc(buffer_size=buffer_size, **kw)
+        h = ctypes.c_void_p()
+        check(lib().mgx_plan_create(ctypes.byref(self.desc), ctypes.byref(h)))
+        self._h = h
+        self.n = buffer_size
+        self.scalar_dtype = np.float64 if kw.get("scalar_f64") else np.float32
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mgx_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------- device (torch)
+    def alloc_outputs(self, num_frames, features, device="cuda"):
+        """Allocate torch device tensors for the requested features; returns (dict, Outputs)."""
+        import torch
+        st = torch.float64 if self.scalar_dtype == np.float64 else torch.float32
+        L = self.n // 2
+        out, o = {}, Outputs()
+        for f in features:
+            if f in SCALAR_NAMES:
+                out[f] = torch.empty(num_frames, dtype=st, device=device)
+                o.scalars[SCALAR_NAMES.index(f)] = out[f].data_ptr()
+            elif f == "loudness":
+                out["loudness.specific"] = torch.empty(num_frames, NUM_BARK, dtype=torch.float32, device=device)
+                o.loudness_specific = out["loudness.specific"].data_ptr()
+                out["loudness.total"] = torch.empty(num_frames, dtype=st, device=device)
+                o.scalars[10] = out["loudness.total"].data_ptr()
+            elif f == "mfcc":
+                out[f] = torch.empty(num_frames, self.desc.num_mfcc_coeffs, dtype=torch.float32, device=device)
+                o.mfcc = out[f].data_ptr()
+            elif f == "amplitudeSpectrum":
+                out[f] = torch.empty(num_frames, L, dtype=torch.float32, device=device)
+                o.amplitude_spectrum = out[f].data_ptr()
+            elif f == "powerSpectrum":
+                out[f] = torch.empty(num_frames, L, dtype=torch.float32, device=device)
+                o.power_spectrum = out[f].data_ptr()
+            elif f == "complexSpectrum":
+                out["complexSpectrum.real"] = torch.empty(num_frames, self.n, dtype=torch.float32, device=device)
+                out["complexSpectrum.imag"] = torch.empty(num_frames, self.n, dtype=torch.float32, device=device)
+                o.complex_real = out["complexSpectrum.real"].data_ptr()
+                o.complex_imag = out["complexSpectrum.imag"].data_ptr()
+            else:
+                raise ValueError("unknown feature %r" % f)
+        return out, o
+
+    def extract_device(self, frames_ptr, num_frames, outputs, stream=None):
+        """Launch on device pointers (async on `stream`, an int hipStream_t handle or None)."""
+        check(lib().mgx_extract_device(self._h, ctypes.c_void_p(frames_ptr), num_frames,
+                                       ctypes.byref(outputs), ctypes.c_void_p(stream or 0)))
+
+    def extract_torch(self, frames, features, stream=None):
+        """frames: a (F, N) float32 CUDA tensor. Returns a dict of device tensors."""
+        import torch
+        assert frames.is_cuda and frames.dtype == torch.float32 and frames.is_contiguous()
+        assert frames.dim() == 2 and frames.shape[1] == self.n
+        out, o = self.alloc_outputs(frames.shape[0], features, device=frames.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(frames.device).cuda_stream
+        self.extract_device(frames.data_ptr(), frames.shape[0], o, stream)
+        return out
+
+    # ------------------------------------------------------------------ host
+    def extract(self, frames, features):
+        """Host numpy in / numpy out (stages through the device)."""
+        frames = np.ascontiguousarray(frames, dtype=np.float32)
+        F, n = frames.shape
+        assert n == self.n
+        L = n // 2
+        out, o = {}, Outputs()
+        sd = self.scalar_dtype
+        for f in features:
+            if f in SCALAR_NAMES:
+                out[f] = np.empty(F, sd)
+                o.scalars[SCALAR_NAMES.index(f)] = out[f].ctypes.data
+            elif f == "loudness":
+                out["loudness.specific"] = np.empty((F, NUM_BARK), np.float32)
+                out["loudness.total"] = np.empty(F, sd)
+                o.loudness_specific = out["loudness.specific"].ctypes.data
+                o.scalars[10] = out["loudness.total"].ctypes.data
+            elif f == "mfcc":
+                out[f] = np.empty((F, self.desc.num_mfcc_coeffs), np.float32)
+                o.mfcc = out[f].ctypes.data
+            elif f == "amplitudeSpectrum":
+                out[f] = np.empty((F, L), np.float32)
+                o.amplitude_spectrum = out[f].ctypes.data
+            elif f == "powerSpectrum":
+                out[f] = np.empty((F, L), np.float32)
+                o.power_spectrum = out[f].ctypes.data
+            elif f == "complexSpectrum":
+                out["complexSpectrum.real"] = np.empty((F, n), np.float32)
+                out["complexSpectrum.imag"] = np.empty((F, n), np.float32)
+                o.complex_real = out["complexSpectrum.real"].ctypes.data
+                o.complex_imag = out["complexSpectrum.imag"].ctypes.data
+            else:
+                raise ValueError("unknown feature %r" % f)
+        check(lib().mgx_extract_host(self._h, frames.ctypes.data, F, ctypes.byref(o)))
+        return out
+
+
+ALL_FEATURES = SCALAR_NAMES[:10] + ["loudness", "perceptualSpread", "perceptualSharpness", "mfcc"]
+
+
+def synth_frames_device(tensor, seed, first_frame=0, stream=None):
+    """Fill a (F, N) float32 CUDA tensor with the synthetic PCM of SURVEY.md §8(d)."""
+    import torch
+    F, n = tensor.shape
+    if stream is None:
+        stream = torch.cuda.current_stream(tensor.device).cuda_stream
+    check(lib().mgx_synth_frames_device(ctypes.c_void_p(tensor.data_ptr()), F, n, seed, first_frame,
+                                        ctypes.c_void_p(stream)))

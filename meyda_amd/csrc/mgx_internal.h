@@ -1,0 +1,55 @@
+// Internal definitions shared by the host plan code and the HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/meyda_gpu.h"
+
+namespace mgx {
+
+constexpr int kMaxMel = 64;
+constexpr int kBark = 24;
+constexpr int kMaxCoeffs = 32;
+constexpr int kThreads = 256;  // 4 waves per workgroup
+
+// Device-resident, read-only tables of a plan (one allocation, see plan.cpp).
+struct DevTables {
+  const float* window;       // N, the selected window (src/meyda.js:116-138)
+  const double2* tw;         // N/2 - 1 faithful twiddles, stage q at offset 2^q - 1
+  const float2* twf;         // same, float32 (MGX_PRECISION_FAST)
+  const int* klist;          // N/2: slot location -> spectrum bin
+  const int* bblim;          // 25 bark band limits (loudness.js:24-45)
+  const int* mel_start;      // per filter: first bin of its support (clipped to [0, N/2))
+  const int* mel_cnt;        // per filter: support length
+  const int* mel_off;        // per filter: offset into mel_w
+  const double* mel_w;       // filterbank weights on the support (mfcc.js:40-51)
+  const float* dct;          // ncoef * nfilt, dct[c + j*ncoef] (mfcc.js:67-83)
+  const double* sharp_tail;  // 24: 0.066*exp(0.171*(i+1)) for i >= 15 (perceptualSharpness.js:10)
+};
+
+struct KernelArgs {
+  const float* frames;
+  uint64_t num_frames;
+  DevTables t;
+  mgx_outputs out;
+  double sample_rate;
+  double freq_sum;       // spectralSlope.js: sum of i*sr/N, i < N/2 (input independent)
+  double pow_freq_sum;   // spectralSlope.js: sum of (i*sr/N)^2
+  double nyq_bin;        // spectralRolloff.js:4: sr / (2 (N/2 - 1))
+  int nfilt;
+  int ncoef;
+  int scalar_f64;
+  int need_spectrum;     // any spectral output requested
+  int need_loudness;     // loudness / perceptual outputs requested
+  int need_mfcc;
+};
+
+// Launchers (kernels.hip).
+hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, int grid,
+                          hipStream_t stream);
+hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t first_index,
+                        hipStream_t stream);
+size_t extract_lds_bytes(int n);
+int frames_per_batch(int n);
+
+}  // namespace mgx

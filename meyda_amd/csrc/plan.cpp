@@ -1,0 +1,480 @@
+// Host side of the C ABI (include/meyda_gpu.h): plan construction, host tables,
+// device residency, launches and error reporting.
+//
+// Host tables follow the reference formulas evaluated in IEEE double exactly as
+// the JavaScript does (this file is compiled with -ffp-contract=off); the
+// golden tests compare them bit-for-bit with the reference's own tables
+// (tests/test_capi_host.py).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mgx_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  const int code = (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? MGX_E_OUT_OF_MEMORY : MGX_E_DEVICE;
+  return fail(code, "%s: %s", what, hipGetErrorString(e));
+}
+
+const double kJsPi = 3.141592653589793;        // Math.PI
+const double kJsSqrt1_2 = 0.7071067811865476;  // Math.SQRT1_2
+
+const char* const kNames[MGX_NUM_FEATURES] = {
+    "rms", "energy", "zcr", "spectralCentroid", "spectralFlatness", "spectralSlope",
+    "spectralRolloff", "spectralSpread", "spectralSkewness", "spectralKurtosis",
+    "loudness.total", "perceptualSpread", "perceptualSharpness", "loudness", "mfcc",
+    "amplitudeSpectrum", "powerSpectrum", "complexSpectrum", "buffer"};
+
+// src/feature-info.js:1-65
+const int kInfo[MGX_NUM_FEATURES] = {
+    MGX_TYPE_NUMBER, MGX_TYPE_NUMBER, MGX_TYPE_NUMBER, MGX_TYPE_NUMBER, MGX_TYPE_NUMBER,
+    MGX_TYPE_NUMBER, MGX_TYPE_NUMBER, MGX_TYPE_NUMBER, MGX_TYPE_NUMBER, MGX_TYPE_NUMBER,
+    MGX_TYPE_NUMBER, MGX_TYPE_NUMBER, MGX_TYPE_NUMBER, MGX_TYPE_MULTIPLE_ARRAYS, MGX_TYPE_ARRAY,
+    MGX_TYPE_ARRAY, MGX_TYPE_ARRAY, MGX_TYPE_MULTIPLE_ARRAYS, MGX_TYPE_ARRAY};
+
+// --------------------------------------------------------------- host tables
+// src/meyda.js:128-138
+void hanning(int n, float* out) {
+  for (int i = 0; i < n; i++) out[i] = (float)(0.5 - 0.5 * cos(2 * kJsPi * i / (n - 1)));
+}
+// src/meyda.js:116-126
+void hamming(int n, float* out) {
+  for (int i = 0; i < n; i++) out[i] = (float)(0.54 - 0.46 * cos(2 * kJsPi * ((double)i / n - 1)));
+}
+// src/meyda.js:170-182 (the frequency is stored to a Float32Array, then read back)
+void bark_scale(int n, double sr, float* out) {
+  for (int i = 0; i < n; i++) {
+    const float f = (float)((double)i * sr / n);
+    const double q = (double)f / 7518;
+    out[i] = (float)(13 * atan((double)f / 1315.8) + 3.5 * atan(q * q));
+  }
+}
+// src/extractors/loudness.js:24-45
+void bark_limits(const float* bark, int len, int nb, int32_t* lim) {
+  double end = (double)bark[len - 1] / nb;
+  int band = 1;
+  for (int i = 0; i <= nb; i++) lim[i] = 0;
+  for (int i = 0; i < len; i++) {
+    while ((double)bark[i] > end) {
+      if (band <= nb) lim[band] = i;
+      band++;
+      end = (double)band * bark[len - 1] / nb;
+    }
+  }
+  lim[nb] = len - 1;
+}
+// src/extractors/mfcc.js:7-38
+void mel_bins(int n, double sr, int nf, int32_t* bins) {
+  const double lo = 1125 * log(1 + (0.0 / 700));
+  const double hi = 1125 * log(1 + ((sr / 2) / 700));
+  const double step = (hi - lo) / (nf + 1);
+  for (int i = 0; i < nf + 2; i++) {
+    const float mv = (float)(i * step);
+    const float mf = (float)(700 * (exp((double)mv / 1125) - 1));
+    bins[i] = (int32_t)floor((double)(n + 1) * mf / sr);
+  }
+}
+// src/extractors/mfcc.js:67-83
+void dct_table(int nf, int nc, float* dct) {
+  const double k = kJsPi / nf, w1 = 1.0 / sqrt((double)nf), w2 = sqrt(2.0 / nf);
+  for (int i = 0; i < nc; i++)
+    for (int j = 0; j < nf; j++) dct[i + j * nc] = (float)((i == 0 ? w1 : w2) * cos(k * (i + 1) * (j + 0.5)));
+}
+// Logical Hermitian index stored at each slot location of a size-m block.
+void klist(int m, std::vector<int>& k) {
+  k.assign(m / 2, 0);
+  if (m == 2) return;
+  std::vector<int> sub;
+  klist(m / 2, sub);
+  const int w = m / 2, h = w / 2;
+  k[0] = 0;
+  k[h] = w / 2;
+  for (int a = 1; a < h; a++) {
+    k[a] = sub[a];
+    k[h + a] = w - sub[a];
+  }
+}
+// lib/jsfft/fft.js:140-165: per stage, f_j by the recurrence from (cos pi/w, sin pi/w).
+// Entry a of stage q (input blocks of w = 2^(q+1) samples): a = 0 holds f_{w/2}
+// (unscaled, for the block-start pair); a > 0 holds SQRT1_2 * f_{k(a)}.
+void twiddles(int n, std::vector<double>& tw) {
+  const int L = n / 2;
+  tw.assign(2 * (size_t)(L > 1 ? L - 1 : 0), 0.0);
+  size_t off = 0;
+  for (int w = 2; w <= L; w <<= 1) {
+    const int h = w / 2;
+    const double dr = cos(kJsPi / w), di = sin(kJsPi / w);
+    std::vector<double> fr(w), fi(w);
+    double r = 1, i = 0;
+    for (int j = 0; j < w; j++) {
+      fr[j] = r;
+      fi[j] = i;
+      const double t = r * dr - i * di;
+      i = r * di + i * dr;
+      r = t;
+    }
+    std::vector<int> kl;
+    klist(w, kl);
+    for (int a = 0; a < h; a++) {
+      const int k = a == 0 ? w / 2 : kl[a];
+      const double sc = a == 0 ? 1.0 : kJsSqrt1_2;
+      tw[2 * (off + a)] = sc * fr[k];
+      tw[2 * (off + a) + 1] = sc * fi[k];
+    }
+    off += h;
+  }
+}
+
+int validate(const mgx_plan_desc* d) {
+  if (!d) return fail(MGX_E_INVALID_ARGUMENT, "plan descriptor is NULL");
+  if (d->struct_size != sizeof(mgx_plan_desc))
+    return fail(MGX_E_INVALID_ARGUMENT, "mgx_plan_desc.struct_size is %u, expected %zu", d->struct_size, sizeof(mgx_plan_desc));
+  if (!mgx_is_power_of_two((double)d->buffer_size))
+    return fail(MGX_E_NOT_POWER_OF_TWO, "Buffer size is not a power of two: Meyda will not run.");
+  if (!(d->sample_rate > 0) || !std::isfinite(d->sample_rate))
+    return fail(MGX_E_INVALID_ARGUMENT, "sample_rate must be positive and finite");
+  if (d->window > MGX_WINDOW_HAMMING) return fail(MGX_E_INVALID_ARGUMENT, "unknown window %u", d->window);
+  if (d->precision > MGX_PRECISION_FAST) return fail(MGX_E_INVALID_ARGUMENT, "unknown precision %u", d->precision);
+  if (d->mode > MGX_MODE_LITERAL) return fail(MGX_E_INVALID_ARGUMENT, "unknown mode %u", d->mode);
+  if (d->num_bark_bands != mgx::kBark) return fail(MGX_E_UNSUPPORTED, "num_bark_bands must be 24 (loudness.js)");
+  if (d->num_mel_bands < 1 || d->num_mel_bands > (uint32_t)mgx::kMaxMel)
+    return fail(MGX_E_UNSUPPORTED, "num_mel_bands must be in [1, %d]", mgx::kMaxMel);
+  if (d->num_mfcc_coeffs < 1 || d->num_mfcc_coeffs > (uint32_t)mgx::kMaxCoeffs)
+    return fail(MGX_E_UNSUPPORTED, "num_mfcc_coeffs must be in [1, %d]", mgx::kMaxCoeffs);
+  return MGX_OK;
+}
+
+template <typename T>
+size_t carve(size_t& off, size_t count) {
+  off = (off + 255) / 256 * 256;
+  const size_t at = off;
+  off += count * sizeof(T);
+  return at;
+}
+
+}  // namespace
+
+struct mgx_plan {
+  mgx_plan_desc d;
+  int n = 0, L = 0;
+  unsigned char* dev = nullptr;
+  mgx::DevTables t{};
+  double freq_sum = 0, pow_freq_sum = 0, nyq = 0;
+  int grid_cap = 1;
+  // staging for mgx_extract_host
+  float* s_frames = nullptr;
+  unsigned char* s_out = nullptr;
+  size_t s_out_bytes = 0;
+  uint64_t s_chunk = 0;
+};
+
+extern "C" {
+
+int mgx_abi_version(void) { return MGX_ABI_VERSION; }
+const char* mgx_last_error(void) { return g_last_error.c_str(); }
+
+// src/utils.js:13-19
+int mgx_is_power_of_two(double num) {
+  while (fmod(num, 2.0) == 0.0 && num > 1) num /= 2;
+  return num == 1;
+}
+
+int mgx_feature_index(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < MGX_NUM_FEATURES; ++i)
+    if (strcmp(name, kNames[i]) == 0) return i;
+  return -1;
+}
+const char* mgx_feature_name(int f) { return (f >= 0 && f < MGX_NUM_FEATURES) ? kNames[f] : nullptr; }
+int mgx_feature_info(int f) { return (f >= 0 && f < MGX_NUM_FEATURES) ? kInfo[f] : -1; }
+
+void mgx_plan_desc_init(mgx_plan_desc* d) {
+  if (!d) return;
+  memset(d, 0, sizeof *d);
+  d->struct_size = sizeof *d;
+  d->buffer_size = 512;
+  d->sample_rate = 44100.0;
+  d->window = MGX_WINDOW_HANNING;
+  d->precision = MGX_PRECISION_FAITHFUL;
+  d->mode = MGX_MODE_PER_BUFFER_FFT;
+  d->num_bark_bands = 24;
+  d->num_mel_bands = 26;
+  d->num_mfcc_coeffs = 13;
+  d->scalar_f64 = 0;
+  d->device = 0;
+}
+
+int mgx_device_count(int* count) {
+  if (!count) return fail(MGX_E_INVALID_ARGUMENT, "count is NULL");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) c = 0;
+  *count = c;
+  return MGX_OK;
+}
+
+int mgx_get_host_tables(const mgx_plan_desc* d, const mgx_host_tables* out) {
+  int rc = validate(d);
+  if (rc) return rc;
+  if (!out) return fail(MGX_E_INVALID_ARGUMENT, "tables is NULL");
+  const int n = (int)d->buffer_size, nf = (int)d->num_mel_bands, nc = (int)d->num_mfcc_coeffs;
+  std::vector<float> han(n), ham(n), bark(n);
+  hanning(n, han.data());
+  hamming(n, ham.data());
+  bark_scale(n, d->sample_rate, bark.data());
+  if (out->hanning) memcpy(out->hanning, han.data(), n * sizeof(float));
+  if (out->hamming) memcpy(out->hamming, ham.data(), n * sizeof(float));
+  if (out->window) memcpy(out->window, d->window == MGX_WINDOW_HAMMING ? ham.data() : han.data(), n * sizeof(float));
+  if (out->bark_scale) memcpy(out->bark_scale, bark.data(), n * sizeof(float));
+  if (out->bark_limits) bark_limits(bark.data(), n / 2, mgx::kBark, out->bark_limits);
+  if (out->mel_bins) mel_bins(n, d->sample_rate, nf, out->mel_bins);
+  if (out->dct) dct_table(nf, nc, out->dct);
+  return MGX_OK;
+}
+
+int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
+  if (!out) return fail(MGX_E_INVALID_ARGUMENT, "out_plan is NULL");
+  *out = nullptr;
+  int rc = validate(d);
+  if (rc) return rc;
+  const int n = (int)d->buffer_size;
+  if (n < 256 || n > 2048)
+    return fail(MGX_E_UNSUPPORTED, "buffer_size %d: the GPU path supports 256..2048", n);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MGX_E_NO_DEVICE, "no HIP device available");
+  if (d->device < 0 || d->device >= ndev) return fail(MGX_E_INVALID_ARGUMENT, "device %d out of range (%d devices)", d->device, ndev);
+  hipError_t e = hipSetDevice(d->device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, d->device);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(MGX_E_NO_DEVICE, "device %d is %s; this build targets gfx950 (MI355X)", d->device, prop.gcnArchName);
+
+  const int L = n / 2, nf = (int)d->num_mel_bands, nc = (int)d->num_mfcc_coeffs;
+  std::vector<float> han(n), ham(n), bark(n), dct((size_t)nc * nf);
+  hanning(n, han.data());
+  hamming(n, ham.data());
+  bark_scale(n, d->sample_rate, bark.data());
+  int32_t lim[mgx::kBark + 1];
+  bark_limits(bark.data(), L, mgx::kBark, lim);
+  std::vector<int32_t> bins(nf + 2);
+  mel_bins(n, d->sample_rate, nf, bins.data());
+  dct_table(nf, nc, dct.data());
+  std::vector<double> tw;
+  twiddles(n, tw);
+  std::vector<float> twf(tw.size());
+  for (size_t i = 0; i < tw.size(); ++i) twf[i] = (float)tw[i];
+  std::vector<int> kl;
+  klist(n, kl);
+  // mel filterbank supports (mfcc.js:40-51), clipped to the bins the sum reads (j < N/2)
+  std::vector<int> mstart(nf), mcnt(nf), moff(nf);
+  std::vector<double> mw;
+  for (int j = 0; j < nf; ++j) {
+    const int lo = std::max(0, (int)bins[j]), hi = std::min(L, (int)bins[j + 2]);
+    mstart[j] = lo;
+    moff[j] = (int)mw.size();
+    for (int i = lo; i < hi; ++i) {
+      double w = 0.0;
+      if (i >= bins[j] && i < bins[j + 1]) w = (double)(i - bins[j]) / (bins[j + 1] - bins[j]);
+      else if (i >= bins[j + 1] && i < bins[j + 2]) w = (double)(bins[j + 2] - i) / (bins[j + 2] - bins[j + 1]);
+      mw.push_back(w);
+    }
+    mcnt[j] = std::max(0, hi - lo);
+  }
+  if (mw.empty()) mw.push_back(0.0);
+  double tail[mgx::kBark];
+  for (int i = 0; i < mgx::kBark; ++i) tail[i] = i < 15 ? 0.0 : 0.066 * exp(0.171 * (i + 1));
+
+  auto* p = new mgx_plan();
+  p->d = *d;
+  p->n = n;
+  p->L = L;
+  // spectralSlope.js:9-16 input-independent sums, in the reference's order
+  for (int i = 0; i < L; i++) {
+    const double f = (double)i * d->sample_rate / n;
+    p->pow_freq_sum += f * f;
+    p->freq_sum += f;
+  }
+  p->nyq = d->sample_rate / (2.0 * (L - 1));  // spectralRolloff.js:4
+  p->grid_cap = prop.multiProcessorCount * 8;
+
+  size_t off = 0;
+  const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
+               o_twf = carve<float>(off, twf.size()), o_kl = carve<int>(off, L),
+               o_lim = carve<int>(off, mgx::kBark + 1), o_ms = carve<int>(off, nf),
+               o_mc = carve<int>(off, nf), o_mo = carve<int>(off, nf), o_mw = carve<double>(off, mw.size()),
+               o_dct = carve<float>(off, dct.size()), o_tail = carve<double>(off, mgx::kBark);
+  std::vector<unsigned char> host(off, 0);
+  auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) memcpy(host.data() + at, src, bytes); };
+  put(o_win, d->window == MGX_WINDOW_HAMMING ? ham.data() : han.data(), n * sizeof(float));
+  put(o_tw, tw.data(), tw.size() * sizeof(double));
+  put(o_twf, twf.data(), twf.size() * sizeof(float));
+  put(o_kl, kl.data(), L * sizeof(int));
+  put(o_lim, lim, sizeof lim);
+  put(o_ms, mstart.data(), nf * sizeof(int));
+  put(o_mc, mcnt.data(), nf * sizeof(int));
+  put(o_mo, moff.data(), nf * sizeof(int));
+  put(o_mw, mw.data(), mw.size() * sizeof(double));
+  put(o_dct, dct.data(), dct.size() * sizeof(float));
+  put(o_tail, tail, sizeof tail);
+  e = hipMalloc(reinterpret_cast<void**>(&p->dev), off);
+  if (e != hipSuccess) { delete p; return hip_fail(e, "hipMalloc(plan tables)"); }
+  e = hipMemcpy(p->dev, host.data(), off, hipMemcpyHostToDevice);
+  if (e != hipSuccess) { (void)hipFree(p->dev); delete p; return hip_fail(e, "hipMemcpy(plan tables)"); }
+  unsigned char* b = p->dev;
+  p->t.window = reinterpret_cast<const float*>(b + o_win);
+  p->t.tw = reinterpret_cast<const double2*>(b + o_tw);
+  p->t.twf = reinterpret_cast<const float2*>(b + o_twf);
+  p->t.klist = reinterpret_cast<const int*>(b + o_kl);
+  p->t.bblim = reinterpret_cast<const int*>(b + o_lim);
+  p->t.mel_start = reinterpret_cast<const int*>(b + o_ms);
+  p->t.mel_cnt = reinterpret_cast<const int*>(b + o_mc);
+  p->t.mel_off = reinterpret_cast<const int*>(b + o_mo);
+  p->t.mel_w = reinterpret_cast<const double*>(b + o_mw);
+  p->t.dct = reinterpret_cast<const float*>(b + o_dct);
+  p->t.sharp_tail = reinterpret_cast<const double*>(b + o_tail);
+  *out = p;
+  return MGX_OK;
+}
+
+int mgx_plan_destroy(mgx_plan* p) {
+  if (!p) return MGX_OK;
+  (void)hipSetDevice(p->d.device);
+  if (p->dev) (void)hipFree(p->dev);
+  if (p->s_frames) (void)hipFree(p->s_frames);
+  if (p->s_out) (void)hipFree(p->s_out);
+  delete p;
+  return MGX_OK;
+}
+
+int mgx_plan_get_desc(const mgx_plan* p, mgx_plan_desc* out) {
+  if (!p || !out) return fail(MGX_E_INVALID_ARGUMENT, "NULL argument");
+  *out = p->d;
+  return MGX_OK;
+}
+
+int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o, void* stream) {
+  if (!p || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL plan or outputs");
+  if (nframes == 0) return MGX_OK;
+  if (!frames) return fail(MGX_E_INVALID_ARGUMENT, "frames is NULL");
+  if ((o->complex_real == nullptr) != (o->complex_imag == nullptr))
+    return fail(MGX_E_INVALID_ARGUMENT, "complex_real and complex_imag must be given together");
+  mgx::KernelArgs a{};
+  a.frames = frames;
+  a.num_frames = nframes;
+  a.t = p->t;
+  a.out = *o;
+  a.sample_rate = p->d.sample_rate;
+  a.freq_sum = p->freq_sum;
+  a.pow_freq_sum = p->pow_freq_sum;
+  a.nyq_bin = p->nyq;
+  a.nfilt = (int)p->d.num_mel_bands;
+  a.ncoef = (int)p->d.num_mfcc_coeffs;
+  a.scalar_f64 = (int)p->d.scalar_f64;
+  bool spec = o->loudness_specific || o->mfcc || o->amplitude_spectrum || o->power_spectrum || o->complex_real;
+  for (int i = MGX_SPECTRAL_CENTROID; i < MGX_NUM_SCALARS; ++i) spec = spec || o->scalars[i];
+  a.need_spectrum = spec;
+  a.need_loudness = o->loudness_specific || o->scalars[MGX_LOUDNESS_TOTAL] || o->scalars[MGX_PERCEPTUAL_SPREAD] ||
+                    o->scalars[MGX_PERCEPTUAL_SHARPNESS];
+  a.need_mfcc = o->mfcc != nullptr;
+  const uint64_t fb = (uint64_t)mgx::frames_per_batch(p->n);
+  const uint64_t nb = (nframes + fb - 1) / fb;
+  const int grid = (int)std::min<uint64_t>(nb, (uint64_t)p->grid_cap);
+  hipError_t e = hipSetDevice(p->d.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "extract kernel launch");
+  return MGX_OK;
+}
+
+int mgx_extract_host(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o) {
+  if (!p || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL plan or outputs");
+  if (nframes == 0) return MGX_OK;
+  if (!frames) return fail(MGX_E_INVALID_ARGUMENT, "frames is NULL");
+  const int n = p->n, L = p->L;
+  const size_t ss = p->d.scalar_f64 ? 8 : 4;
+  const size_t nb = mgx::kBark, nc = p->d.num_mfcc_coeffs;
+  // device bytes per frame for the requested outputs
+  size_t per = 0;
+  for (int i = 0; i < MGX_NUM_SCALARS; ++i) per += o->scalars[i] ? ss : 0;
+  per += (o->loudness_specific ? nb * 4 : 0) + (o->mfcc ? nc * 4 : 0) + (o->amplitude_spectrum ? L * 4 : 0) +
+         (o->power_spectrum ? L * 4 : 0) + (o->complex_real ? 2 * (size_t)n * 4 : 0);
+  const uint64_t chunk = std::min<uint64_t>(nframes, 65536);
+  hipError_t e = hipSetDevice(p->d.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if (p->s_chunk < chunk || p->s_out_bytes < per * chunk + 4096) {
+    if (p->s_frames) (void)hipFree(p->s_frames);
+    if (p->s_out) (void)hipFree(p->s_out);
+    p->s_frames = nullptr;
+    p->s_out = nullptr;
+    p->s_chunk = 0;
+    p->s_out_bytes = 0;
+    e = hipMalloc(reinterpret_cast<void**>(&p->s_frames), chunk * n * sizeof(float));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging frames)");
+    const size_t ob = per * chunk + 4096;
+    e = hipMalloc(reinterpret_cast<void**>(&p->s_out), ob);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging outputs)");
+    p->s_chunk = chunk;
+    p->s_out_bytes = ob;
+  }
+  for (uint64_t f0 = 0; f0 < nframes; f0 += chunk) {
+    const uint64_t cnt = std::min<uint64_t>(chunk, nframes - f0);
+    e = hipMemcpy(p->s_frames, frames + f0 * n, cnt * n * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(frames)");
+    mgx_outputs d{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) { unsigned char* q = p->s_out + off; off += (bytes + 255) / 256 * 256; return q; };
+    for (int i = 0; i < MGX_NUM_SCALARS; ++i) d.scalars[i] = o->scalars[i] ? take(cnt * ss) : nullptr;
+    d.loudness_specific = o->loudness_specific ? reinterpret_cast<float*>(take(cnt * nb * 4)) : nullptr;
+    d.mfcc = o->mfcc ? reinterpret_cast<float*>(take(cnt * nc * 4)) : nullptr;
+    d.amplitude_spectrum = o->amplitude_spectrum ? reinterpret_cast<float*>(take(cnt * L * 4)) : nullptr;
+    d.power_spectrum = o->power_spectrum ? reinterpret_cast<float*>(take(cnt * L * 4)) : nullptr;
+    d.complex_real = o->complex_real ? reinterpret_cast<float*>(take(cnt * n * 4)) : nullptr;
+    d.complex_imag = o->complex_imag ? reinterpret_cast<float*>(take(cnt * n * 4)) : nullptr;
+    int rc = mgx_extract_device(p, p->s_frames, cnt, &d, nullptr);
+    if (rc) return rc;
+    auto back = [&](void* host, const void* dev, size_t bytes) {
+      return host ? hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost) : hipSuccess;
+    };
+    for (int i = 0; i < MGX_NUM_SCALARS && e == hipSuccess; ++i)
+      if (o->scalars[i]) e = back(static_cast<unsigned char*>(o->scalars[i]) + f0 * ss, d.scalars[i], cnt * ss);
+    if (e == hipSuccess && o->loudness_specific) e = back(o->loudness_specific + f0 * nb, d.loudness_specific, cnt * nb * 4);
+    if (e == hipSuccess && o->mfcc) e = back(o->mfcc + f0 * nc, d.mfcc, cnt * nc * 4);
+    if (e == hipSuccess && o->amplitude_spectrum) e = back(o->amplitude_spectrum + f0 * L, d.amplitude_spectrum, cnt * L * 4);
+    if (e == hipSuccess && o->power_spectrum) e = back(o->power_spectrum + f0 * L, d.power_spectrum, cnt * L * 4);
+    if (e == hipSuccess && o->complex_real) e = back(o->complex_real + f0 * n, d.complex_real, cnt * n * 4);
+    if (e == hipSuccess && o->complex_imag) e = back(o->complex_imag + f0 * n, d.complex_imag, cnt * n * 4);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(outputs)");
+  }
+  return MGX_OK;
+}
+
+int mgx_synth_frames_device(float* frames, uint64_t nframes, uint32_t n, uint64_t seed, uint64_t first_frame, void* stream) {
+  if (!frames && nframes) return fail(MGX_E_INVALID_ARGUMENT, "frames is NULL");
+  if (nframes == 0) return MGX_OK;
+  hipError_t e = mgx::launch_synth(frames, nframes * (uint64_t)n, seed, first_frame * (uint64_t)n, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "synth kernel launch");
+  return MGX_OK;
+}
+
+}  // extern "C"

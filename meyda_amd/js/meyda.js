@@ -1,0 +1,247 @@
+'use strict';
+// Meyda-compatible JavaScript facade over the MI355X engine.
+//
+// Same surface as the reference class (src/meyda.js:15-263):
+//   new Meyda(audioContext, source, bufferSize, callback)      src/meyda.js:17-97
+//   get(feature | features[])                                  :244-261
+//   start(features) / stop()                                   :233-241
+//   setSource(source)                                          :229-231
+//   featureInfo, windowingFunction, hanning, hamming, barkScale, signal
+// plus, for the batched engine:
+//   process(signal)                 push one buffer (what onaudioprocess does, :69-91)
+//   getBatch(features, frames)      frames: Float32Array(F * bufferSize) -> SoA typed arrays
+//   getBatchAsync(features, frames) same, off the JS thread (napi_async_work)
+//
+// Every built-in feature is computed by libmeyda_gpu.so through the N-API addon.
+// Differences from the snapshot (documented in INTEGRATION.md): the FFT runs per
+// buffer (the snapshot never transforms, src/meyda.js:79-84; opt back in with
+// {mode: 'literal'}), all 18 extractors are registered (src/extractors/index.js
+// enables only loudness), the callback works (src/meyda.js:87 references an
+// undefined global), and get() returns fresh arrays rather than internal buffers.
+const path = require('path');
+
+const addon = require(process.env.MEYDA_AMD_ADDON ||
+  path.join(__dirname, '..', 'addon', 'meyda_napi.node'));
+const FEATURE_INFO = require('./feature-info');
+
+const GPU_FEATURES = new Set(['rms', 'energy', 'zcr', 'spectralCentroid', 'spectralFlatness',
+  'spectralSlope', 'spectralRolloff', 'spectralSpread', 'spectralSkewness', 'spectralKurtosis',
+  'perceptualSpread', 'perceptualSharpness', 'loudness', 'mfcc', 'amplitudeSpectrum',
+  'powerSpectrum', 'complexSpectrum']);
+
+// src/utils.js:13-19
+function isPowerOfTwo(num) {
+  while (((num % 2) === 0) && num > 1) num /= 2;
+  return (num == 1); // eslint-disable-line eqeqeq
+}
+
+class Meyda {
+  constructor(audioContext, src, bufSize, callback, options) {
+    // src/meyda.js:20-26: validated in this order, so `bufSize || 256` is unreachable
+    if (!isPowerOfTwo(bufSize)) {
+      throw new Error('Buffer size is not a power of two: Meyda will not run.');
+    }
+    if (!audioContext) {
+      throw new Error("AudioContext wasn't specified: Meyda will not run.");
+    }
+    const bufferSize = bufSize || 256;
+    this.audioContext = audioContext;
+    this.bufferSize = bufferSize;
+    this.sampleRate = audioContext.sampleRate;
+    this.options = Object.assign({
+      precision: 'faithful', mode: 'per_buffer_fft', numMelBands: 26, numMfccCoeffs: 13, device: 0,
+    }, options || {});
+    this.featureExtractors = {}; // user plugins: fn(bufferSize, m) or {process(signal)}
+    this.EXTRACTION_STARTED = false;
+    this._featuresToExtract = null;
+    this._callback = callback;
+    this.windowingFunction = 'hanning';
+    const t = addon.hostTables({ bufferSize, sampleRate: this.sampleRate,
+      numMelBands: this.options.numMelBands, numMfccCoeffs: this.options.numMfccCoeffs });
+    this.barkScale = t.barkScale;
+    this.hanning = t.hanning;
+    this.hamming = t.hamming;
+    this.featureInfo = Object.assign({}, FEATURE_INFO);
+    this.signal = null;
+    this._plans = {};
+    this._frame = null; // results of the current buffer, filled lazily by get()
+    // Web Audio wiring when the context provides it (src/meyda.js:67-94). One node per
+    // instance (the reference stored it on a window global).
+    if (typeof audioContext.createScriptProcessor === 'function') {
+      this.spn = audioContext.createScriptProcessor(bufferSize, 1, 1);
+      this.spn.onaudioprocess = (e) => this.process(e.inputBuffer.getChannelData(0));
+      if (typeof this.spn.connect === 'function' && audioContext.destination) {
+        this.spn.connect(audioContext.destination);
+      }
+      if (src && typeof src.connect === 'function') src.connect(this.spn, 0, 0);
+    }
+  }
+
+  // One plan per window type, created on first use (windowingFunction may change at
+  // runtime as in the reference, src/meyda.js:41,76,164).
+  _plan() {
+    const w = this.windowingFunction;
+    if (w !== 'hanning' && w !== 'hamming') {
+      throw new TypeError('unknown windowingFunction "' + w + '"');
+    }
+    if (!this._plans[w]) {
+      this._plans[w] = addon.createPlan({
+        bufferSize: this.bufferSize, sampleRate: this.sampleRate, windowingFunction: w,
+        precision: this.options.precision, mode: this.options.mode,
+        numMelBands: this.options.numMelBands, numMfccCoeffs: this.options.numMfccCoeffs,
+        device: this.options.device, scalarF64: 1,
+      });
+    }
+    return this._plans[w];
+  }
+
+  // The per-buffer handler (src/meyda.js:69-91): take the buffer, then deliver the
+  // started features to the callback.
+  process(signal) {
+    if (!(signal instanceof Float32Array)) signal = Float32Array.from(signal);
+    if (signal.length !== this.bufferSize) {
+      throw new RangeError('buffer length ' + signal.length + ' != bufferSize ' + this.bufferSize);
+    }
+    this.signal = signal;
+    this._frame = null;
+    if (typeof this._callback === 'function' && this.EXTRACTION_STARTED) {
+      this._callback(this.get(this._featuresToExtract));
+    }
+  }
+
+  setSource(_src) {
+    _src.connect(this.spn);
+  }
+
+  start(features) {
+    this._featuresToExtract = features;
+    this.EXTRACTION_STARTED = true;
+  }
+
+  stop() {
+    this._featuresToExtract = null;
+    this.EXTRACTION_STARTED = false;
+  }
+
+  // src/meyda.js:244-261
+  get(feature) {
+    if (typeof feature === 'object') {
+      const names = Array.prototype.slice.call(feature); // null throws, as feature.length does
+      this._compute(names.filter((n) => GPU_FEATURES.has(n) && !this.featureExtractors[n]));
+      const results = {};
+      for (let x = 0; x < names.length; x++) {
+        try {
+          results[names[x]] = this._value(names[x]);
+        } catch (e) {
+          console.error(e);
+        }
+      }
+      return results;
+    } else if (typeof feature === 'string') {
+      return this._value(feature);
+    }
+    throw new Error('Invalid Feature Format');
+  }
+
+  _signal() {
+    return this.signal || new Float32Array(this.bufferSize);
+  }
+
+  // Compute the missing GPU features of the current buffer in one launch.
+  _compute(names) {
+    if (!this._frame) this._frame = {};
+    const need = names.filter((n) => !(n in this._frame));
+    if (!need.length) return;
+    const r = addon.extract(this._plan(), this._signal(), need);
+    for (const n of need) this._frame[n] = frameValue(n, r, 0, this.bufferSize, this.options.numMfccCoeffs);
+  }
+
+  _value(name) {
+    const plugin = this.featureExtractors[name];
+    if (plugin) return this._runPlugin(plugin);
+    if (name === 'buffer') return this._signal();
+    if (!GPU_FEATURES.has(name)) {
+      throw new TypeError("Cannot read property 'process' of undefined (feature '" + name + "')");
+    }
+    this._compute([name]);
+    return this._frame[name];
+  }
+
+  // A user extractor sees the same `m` the reference extractors see
+  // (SURVEY.md §8(b)): signal, ampSpectrum, complexSpectrum, audioContext, featureExtractors.
+  _runPlugin(plugin) {
+    if (typeof plugin.process === 'function') return plugin.process(this._signal());
+    this._compute(['amplitudeSpectrum', 'complexSpectrum', 'loudness']);
+    const m = {
+      signal: this._signal(),
+      ampSpectrum: this._frame.amplitudeSpectrum,
+      complexSpectrum: this._frame.complexSpectrum,
+      audioContext: this.audioContext,
+      featureExtractors: Object.assign({ loudness: () => this._frame.loudness }, this.featureExtractors),
+    };
+    return plugin(this.bufferSize, m);
+  }
+
+  // Batch API: frames is a Float32Array holding F consecutive buffers.
+  getBatch(features, frames) {
+    const names = checkBatchNames(features);
+    return addon.extract(this._plan(), toF32(frames), names);
+  }
+
+  getBatchAsync(features, frames) {
+    const names = checkBatchNames(features);
+    return addon.extractAsync(this._plan(), toF32(frames), names);
+  }
+
+  // Per-frame view of a batch result, in the shapes get() returns.
+  static frame(result, name, index, bufferSize, numMfccCoeffs) {
+    return frameValue(name, result, index, bufferSize, numMfccCoeffs);
+  }
+
+  dispose() {
+    for (const k of Object.keys(this._plans)) addon.destroyPlan(this._plans[k]);
+    this._plans = {};
+  }
+}
+
+function toF32(frames) {
+  return frames instanceof Float32Array ? frames : Float32Array.from(frames);
+}
+
+function checkBatchNames(features) {
+  const names = typeof features === 'string' ? [features] : Array.prototype.slice.call(features);
+  for (const n of names) {
+    if (!GPU_FEATURES.has(n)) throw new TypeError("unknown batch feature '" + n + "'");
+  }
+  return names;
+}
+
+// Slice frame `i` of a SoA batch result into the reference's return shapes
+// (src/feature-info.js): numbers, Float32Array, {specific, total}, {real, imag}.
+function frameValue(name, r, i, n, ncoef) {
+  ncoef = ncoef || 13;
+  const L = n / 2;
+  switch (name) {
+    case 'loudness':
+      return { specific: r['loudness.specific'].slice(i * 24, i * 24 + 24), total: r['loudness.total'][i] };
+    case 'mfcc':
+      return r.mfcc.slice(i * ncoef, i * ncoef + ncoef);
+    case 'amplitudeSpectrum':
+      return r.amplitudeSpectrum.slice(i * L, i * L + L);
+    case 'powerSpectrum':
+      return r.powerSpectrum.slice(i * L, i * L + L);
+    case 'complexSpectrum': {
+      const real = r['complexSpectrum.real'].slice(i * n, i * n + n);
+      const imag = r['complexSpectrum.imag'].slice(i * n, i * n + n);
+      return { real, imag, length: n };
+    }
+    default:
+      return r[name][i];
+  }
+}
+
+module.exports = Meyda;
+module.exports.Meyda = Meyda;
+module.exports.isPowerOfTwo = isPowerOfTwo;
+module.exports.featureInfo = FEATURE_INFO;
+module.exports.addon = addon;

@@ -173,22 +173,26 @@ typedef struct {
 /* One frame. Any output pointer may be NULL. */
 static void oracle_frame(const oracle_ctx* c, const float* x, int literal, float* amp_out,
                          float* cre, float* cim, double* sc, float* loud_spec, float* mfcc_out,
-                         float* work) {
+                         float* work, const float* amp_in) {
   const int n = c->n, L = n / 2;
   float* re = work;          /* n */
   float* im = work + n;      /* n */
   float* amp = work + 2 * n; /* L */
-  /* src/meyda.js:158-168: windowed[i] = sig[i] * w[i] stored to Float32Array */
-  for (int i = 0; i < n; i++) { re[i] = (float)((double)x[i] * c->window[i]); im[i] = 0.0f; }
-  if (!literal) oracle_jsfft(re, im, n); /* literal: the snapshot never transforms per buffer */
-  /* src/meyda.js:104-114 */
-  for (int i = 0; i < L; i++) {
-    double r = re[i], q = im[i];
-    amp[i] = (float)sqrt(r * r + q * q);
+  if (amp_in) {
+    memcpy(amp, amp_in, sizeof(float) * L); /* features of a given spectrum (test helper) */
+  } else {
+    /* src/meyda.js:158-168: windowed[i] = sig[i] * w[i] stored to Float32Array */
+    for (int i = 0; i < n; i++) { re[i] = (float)((double)x[i] * c->window[i]); im[i] = 0.0f; }
+    if (!literal) oracle_jsfft(re, im, n); /* literal: the snapshot never transforms per buffer */
+    /* src/meyda.js:104-114 */
+    for (int i = 0; i < L; i++) {
+      double r = re[i], q = im[i];
+      amp[i] = (float)sqrt(r * r + q * q);
+    }
+    if (amp_out) memcpy(amp_out, amp, sizeof(float) * L);
+    if (cre) memcpy(cre, re, sizeof(float) * n);
+    if (cim) memcpy(cim, im, sizeof(float) * n);
   }
-  if (amp_out) memcpy(amp_out, amp, sizeof(float) * L);
-  if (cre) memcpy(cre, re, sizeof(float) * n);
-  if (cim) memcpy(cim, im, sizeof(float) * n);
   if (!sc && !loud_spec && !mfcc_out) return;
 
   double s[ORACLE_NUM_SCALARS];
@@ -279,11 +283,12 @@ static void oracle_frame(const oracle_ctx* c, const float* x, int literal, float
  * Outputs (each may be NULL): amp F x n/2, cre/cim F x n, scalars F x 13 (record
  * order above), loud_spec F x 24, mfcc F x 13. literal != 0 reproduces the
  * snapshot's onaudioprocess (no per-buffer FFT). Returns 0, or -1 on bad input.
- * Thread-safe: callers may run disjoint frame ranges concurrently.
+ * Thread-safe: callers may run disjoint frame ranges concurrently. amp_in (optional, F x n/2)
+ * replaces the window+FFT+amplitude steps (used to isolate feature parity in tests).
  */
-int oracle_extract(const float* frames, long nframes, int n, double sr, int window, int nfilt,
-                   int literal, float* amp, float* cre, float* cim, double* scalars,
-                   float* loud_spec, float* mfcc) {
+int oracle_extract_ex(const float* frames, const float* amp_in, long nframes, int n, double sr,
+                      int window, int nfilt, int literal, float* amp, float* cre, float* cim,
+                      double* scalars, float* loud_spec, float* mfcc) {
   if (!oracle_is_power_of_two(n) || n < 4 || nfilt < 1 || nfilt > 64) return -1;
   const int L = n / 2;
   float* win = malloc(sizeof(float) * n);
@@ -304,10 +309,24 @@ int oracle_extract(const float* frames, long nframes, int n, double sr, int wind
                  amp ? amp + f * L : NULL, cre ? cre + f * n : NULL, cim ? cim + f * n : NULL,
                  scalars ? scalars + f * ORACLE_NUM_SCALARS : NULL,
                  loud_spec ? loud_spec + f * ORACLE_NUM_BARK : NULL,
-                 mfcc ? mfcc + f * ORACLE_NUM_COEFFS : NULL, work);
+                 mfcc ? mfcc + f * ORACLE_NUM_COEFFS : NULL, work, amp_in ? amp_in + f * L : NULL);
   }
   free(win); free(bark); free(dct); free(work);
   return 0;
+}
+
+int oracle_extract(const float* frames, long nframes, int n, double sr, int window, int nfilt,
+                   int literal, float* amp, float* cre, float* cim, double* scalars,
+                   float* loud_spec, float* mfcc) {
+  return oracle_extract_ex(frames, NULL, nframes, n, sr, window, nfilt, literal, amp, cre, cim,
+                           scalars, loud_spec, mfcc);
+}
+
+/* Features of given amplitude spectra (frames still supply rms/energy/zcr). */
+int oracle_features_from_amp(const float* frames, const float* amp_in, long nframes, int n,
+                             double sr, int nfilt, double* scalars, float* loud_spec, float* mfcc) {
+  return oracle_extract_ex(frames, amp_in, nframes, n, sr, 0, nfilt, 0, NULL, NULL, NULL, scalars,
+                           loud_spec, mfcc);
 }
 
 /* Synthetic PCM: splitmix64 output for state seed advanced

@@ -37,6 +37,9 @@ def lib():
         L.oracle_extract.argtypes = [fp, ctypes.c_long, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, fp, fp, fp, dp, fp, fp]
         L.oracle_extract.restype = ctypes.c_int
+        L.oracle_features_from_amp.argtypes = [fp, fp, ctypes.c_long, ctypes.c_int, ctypes.c_double,
+                                               ctypes.c_int, dp, fp, fp]
+        L.oracle_features_from_amp.restype = ctypes.c_int
         L.oracle_hanning.argtypes = [ctypes.c_int, fp]
         L.oracle_hamming.argtypes = [ctypes.c_int, fp]
         L.oracle_bark_scale.argtypes = [ctypes.c_int, ctypes.c_double, fp]
@@ -77,6 +80,24 @@ def extract(frames, sample_rate=44100.0, window="hanning", num_mel=26, literal=F
                               _p(out["mfcc"]))
     if rc != 0:
         raise ValueError("oracle_extract rejected the arguments (N=%d)" % N)
+    return out
+
+
+def features_from_amp(frames, amp, sample_rate=44100.0, num_mel=26):
+    """Reference features of a given amplitude spectrum (rms/energy/zcr from frames)."""
+    frames = np.ascontiguousarray(frames, dtype=np.float32)
+    amp = np.ascontiguousarray(amp, dtype=np.float32)
+    F, N = frames.shape
+    out = {
+        "scalars": np.empty((F, NUM_SCALARS), np.float64),
+        "loudness_specific": np.empty((F, NUM_BARK), np.float32),
+        "mfcc": np.empty((F, NUM_COEFFS), np.float32),
+    }
+    rc = lib().oracle_features_from_amp(_p(frames), _p(amp), F, N, sample_rate, num_mel,
+                                        _p(out["scalars"], ctypes.c_double),
+                                        _p(out["loudness_specific"]), _p(out["mfcc"]))
+    if rc != 0:
+        raise ValueError("oracle_features_from_amp rejected the arguments")
     return out
 
 

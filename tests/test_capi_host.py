@@ -1,0 +1,101 @@
+"""C-ABI host-side tests (no GPU needed): the library loads, exports every symbol the
+header declares, validates like the reference constructor, and computes the host
+tables bit-for-bit like the reference (tests/golden)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import golden_io
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from meyda_amd import capi
+    capi.lib()
+    return capi
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "meyda_gpu.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mgx_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_exports_every_header_symbol(capi):
+    funcs = header_functions()
+    assert len(funcs) >= 15
+    assert sorted(capi.EXPORTS) == funcs
+    L = capi.lib()
+    for f in funcs:
+        assert hasattr(L, f), f
+
+
+def test_abi_version_and_names(capi):
+    L = capi.lib()
+    assert L.mgx_abi_version() == 1
+    for i, name in enumerate(capi.FEATURE_NAMES):
+        assert L.mgx_feature_name(i).decode() == name
+        assert L.mgx_feature_index(name.encode()) == i
+    assert L.mgx_feature_index(b"nope") == -1
+    assert L.mgx_feature_name(99) is None
+    # src/feature-info.js types: number=0, array=1, multipleArrays=2
+    info = {n: L.mgx_feature_info(i) for i, n in enumerate(capi.FEATURE_NAMES)}
+    assert info["rms"] == 0 and info["mfcc"] == 1 and info["loudness"] == 2
+    assert info["complexSpectrum"] == 2 and info["amplitudeSpectrum"] == 1 and info["buffer"] == 1
+
+
+def test_is_power_of_two_matches_reference(capi):
+    # src/utils.js:13-19 halves while even; 1 is a power of two, 0 and 6 are not.
+    L = capi.lib()
+    for n, want in [(1, 1), (2, 1), (512, 1), (0, 0), (6, 0), (1023, 0), (2.5, 0), (-4, 0)]:
+        assert L.mgx_is_power_of_two(float(n)) == want, n
+
+
+def test_not_power_of_two_is_rejected_first(capi):
+    with pytest.raises(capi.MgxError) as ei:
+        capi.Plan(buffer_size=1000)
+    assert ei.value.status == -2
+    assert "not a power of two" in str(ei.value)
+
+
+def test_bad_descriptor(capi):
+    import ctypes
+    d = capi.make_desc()
+    d.struct_size = 3
+    h = ctypes.c_void_p()
+    assert capi.lib().mgx_plan_create(ctypes.byref(d), ctypes.byref(h)) == -1
+    assert b"struct_size" in capi.lib().mgx_last_error()
+    d = capi.make_desc()
+    d.num_bark_bands = 12
+    assert capi.lib().mgx_plan_create(ctypes.byref(d), ctypes.byref(h)) == -3
+
+
+@pytest.mark.parametrize("n", [512, 1024, 2048])
+def test_host_tables_bit_exact(capi, n):
+    g = golden_io.load(n)
+    t = capi.host_tables(buffer_size=n)
+    assert np.array_equal(t["hanning"].view(np.uint32), g["hann"].view(np.uint32))
+    assert np.array_equal(t["hamming"].view(np.uint32), g["hamming"].view(np.uint32))
+    assert np.array_equal(t["window"].view(np.uint32), g["hann"].view(np.uint32))
+    assert np.array_equal(t["bark_scale"].view(np.uint32), g["bark"].view(np.uint32))
+    assert np.array_equal(t["bark_limits"], g["bblimits"])
+    assert np.array_equal(t["mel_bins"], g["mel_bins"])
+    assert np.array_equal(t["dct"].view(np.uint32), g["dct"].view(np.uint32))
+    t40 = capi.host_tables(buffer_size=n, num_mel_bands=40)
+    assert np.array_equal(t40["mel_bins"], g["mel40_bins"])
+    assert np.array_equal(t40["dct"].view(np.uint32), g["dct40"].view(np.uint32))
+    th = capi.host_tables(buffer_size=n, window="hamming")
+    assert np.array_equal(th["window"].view(np.uint32), g["hamming"].view(np.uint32))
+
+
+def test_no_silent_cpu_fallback(capi):
+    # Without a gfx950 device the plan must fail loudly (no CPU path exists).
+    if capi.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(capi.MgxError) as ei:
+        capi.Plan(buffer_size=1024)
+    assert ei.value.status == -6
