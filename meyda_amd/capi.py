@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmeyda_gpu.so")
+LIB_PATH = os.environ.get("MEYDA_AMD_LIB") or os.path.join(HERE, "libmeyda_gpu.so")
 
 NUM_SCALARS = 13
 NUM_BARK = 24

@@ -3,7 +3,7 @@
 // One launch processes a batch of frames. Each 256-thread workgroup loops over
 // batches of FB frames:
 //
-//  Phase 1 (one wave per frame, FB/4 frames per wave):
+//  Phase 1 (one wave per frame, FB/4 frames per wave, next frame prefetched):
 //    load + rms/energy/zcr      src/extractors/rms.js, energy.js, zcr.js
 //    window                     src/meyda.js:158-168
 //    FFT                        lib/jsfft/fft.js:123-208, restated as a Hermitian
@@ -15,11 +15,13 @@
 //    amplitude                  src/meyda.js:104-114 -> LDS batch buffer
 //    per-frame reductions       moments (src/utils.js:1-11), log sum
 //                               (spectralFlatness.js), prefix sums (spectralRolloff.js,
-//                               loudness band sums loudness.js:47-66)
-//  Phase 2 (whole workgroup, frames x bands in parallel):
-//    specific loudness          loudness.js:55-63 (pow 0.23, float32 store)
-//    mel filterbank + log       mfcc.js:53-65 (sequential float32 accumulation, as written)
-//    DCT                        mfcc.js:85-93
+//                               loudness band sums loudness.js:47-66), DPP wave sums
+//  Phase 2 (whole workgroup, over the batch):
+//    mel filterbank             mfcc.js:40-62 as an MFMA GEMM on the matrix cores
+//                               (v_mfma_f32_16x16x4_f32: 16 bands x 16 frames per tile,
+//                               K = the bins of the tile's banded support)
+//    specific loudness          loudness.js:55-63 (x^0.23, float32 store)
+//    log mel + DCT              mfcc.js:64-93 (double, sequential as written)
 //    scalar features            spectral*.js, perceptual*.js
 //
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit.
@@ -27,6 +29,12 @@
 
 namespace mgx {
 namespace {
+
+typedef const __attribute__((address_space(1))) double2* GTw;
+typedef const __attribute__((address_space(1))) float2* GTwf;
+typedef const __attribute__((address_space(1))) double* GD;
+typedef const __attribute__((address_space(1))) float* GF;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr double kS = 0.7071067811865476;  // Math.SQRT1_2 (lib/jsfft/fft.js:10)
 constexpr float kSf = 0.70710677f;
@@ -47,8 +55,9 @@ struct Geo {
   static constexpr int RB = ilog2c(R);      // register bits
   static constexpr int NPASS = (SB + RB - 1) / RB;
   static constexpr int CH = N / 64;         // 64-sample input chunks per frame
-  static constexpr int FB = N >= 2048 ? 8 : 16;  // frames per workgroup batch
-  static constexpr int AMP_STRIDE = L + 1;  // odd float stride between frames in LDS
+  static constexpr int FB = N >= 1024 ? 8 : 16;  // frames per workgroup batch (<= 16: one MFMA column tile)
+  static constexpr int FPW = FB / 4;        // frames per wave per batch
+  static constexpr int AS = L + 2;          // amplitude row stride: conflict-free MFMA B-operand reads
   static constexpr int SLOT_PHYS = L + (L >> 4) + 2;
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
@@ -88,25 +97,41 @@ struct PassGeo {
 
 __device__ __forceinline__ int phys(int loc) { return loc + (loc >> 4); }
 
+// Wave-level LDS ordering (no global-memory fence: in-flight prefetch loads stay in flight).
 __device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-  return v;
+// Workgroup barrier ordering LDS only. __syncthreads() also fences global memory, which
+// makes every wave drain its outstanding loads (the next frame's prefetch) at each barrier.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
+  const GD q = (GD)p;
+  return make_double2(q[2 * i], q[2 * i + 1]);
+}
+__device__ __forceinline__ float2 ld_twf(GTwf p, int i) {
+  const GF q = (GF)p;
+  return make_float2(q[2 * i], q[2 * i + 1]);
 }
 
 // ---------------------------------------------------------------- butterflies
-// Generic slot pair (location a > 0 in its block), c = SQRT1_2 * f_k:
-//   lo <- s L + c R,  hi <- conj(s L - c R)
+// Twiddle table of stage q (input blocks of 2^(q+1) samples) at offset 2^q - 1:
+// entry a > 0 holds c = SQRT1_2 * f_k(a) for the slot pair (a, a + 2^q); entry 0
+// holds f_{w/2} unscaled for the block-start pair, whose slots pack (X[0], X[w/2]).
+//
+// Generic pair:      lo <- s L + c R,   hi <- conj(s L - c R)
+// Block-start pair:  exactly jsfft's operations for j = 0 and j = w/2.
 template <bool FAITH>
-__device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, const double2* tw, const float2* twf, int idx) {
+__device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, GTw tw, GTwf twf, int idx) {
   if constexpr (FAITH) {
-    const double2 c = tw[idx];
+    const double2 c = ld_tw(tw, idx);
     const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
     const double Ar = __builtin_fma(c.x, Rr, -(c.y * Ri));
     const double Ai = __builtin_fma(c.x, Ri, c.y * Rr);
@@ -115,7 +140,7 @@ __device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, const doubl
     hi.x = (float)__builtin_fma(kS, Lr, -Ar);
     hi.y = (float)__builtin_fma(-kS, Li, Ai);
   } else {
-    const float2 c = twf[idx];
+    const float2 c = ld_twf(twf, idx);
     const float Ar = __builtin_fmaf(c.x, hi.x, -(c.y * hi.y));
     const float Ai = __builtin_fmaf(c.x, hi.y, c.y * hi.x);
     const float Lr = lo.x, Li = lo.y;
@@ -126,19 +151,17 @@ __device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, const doubl
   }
 }
 
-// Block-start pair (location 0): the packed reals (X[0], X[w/2]) of both halves.
-// Exactly jsfft's operations for j = 0 and j = w/2 (f_0 = 1, f = f_{w/2} unscaled).
 template <bool FAITH>
-__device__ __forceinline__ void bfly_special(float2& lo, float2& hi, const double2* tw, const float2* twf, int idx) {
+__device__ __forceinline__ void bfly_special(float2& lo, float2& hi, GTw tw, GTwf twf, int idx) {
   if constexpr (FAITH) {
-    const double2 f = tw[idx];
+    const double2 f = ld_tw(tw, idx);
     const double L0 = lo.x, Lh = lo.y, R0 = hi.x, Rh = hi.y;
     lo.x = (float)(kS * (L0 + R0));
     lo.y = (float)(kS * (L0 - R0));
     hi.x = (float)(kS * (Lh + f.x * Rh));
     hi.y = (float)(kS * (f.y * Rh));
   } else {
-    const float2 f = twf[idx];
+    const float2 f = ld_twf(twf, idx);
     const float L0 = lo.x, Lh = lo.y, R0 = hi.x, Rh = hi.y;
     lo.x = kSf * (L0 + R0);
     lo.y = kSf * (L0 - R0);
@@ -147,9 +170,42 @@ __device__ __forceinline__ void bfly_special(float2& lo, float2& hi, const doubl
   }
 }
 
+// A pair that is block-start on some lanes (sp) and generic on the others: both
+// results are formed branch-free and selected, so the wave never diverges.
+template <bool FAITH>
+__device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf twf, int idx, bool sp) {
+  if constexpr (FAITH) {
+    const double2 c = ld_tw(tw, idx);
+    const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+    const double Ar = __builtin_fma(c.x, Rr, -(c.y * Ri));
+    const double Ai = __builtin_fma(c.x, Ri, c.y * Rr);
+    const double g0 = __builtin_fma(kS, Lr, Ar), g1 = __builtin_fma(kS, Li, Ai);
+    const double g2 = __builtin_fma(kS, Lr, -Ar), g3 = __builtin_fma(-kS, Li, Ai);
+    const double s0 = kS * (Lr + Rr), s1 = kS * (Lr - Rr);
+    const double s2 = kS * (Li + c.x * Ri), s3 = kS * (c.y * Ri);
+    lo.x = (float)(sp ? s0 : g0);
+    lo.y = (float)(sp ? s1 : g1);
+    hi.x = (float)(sp ? s2 : g2);
+    hi.y = (float)(sp ? s3 : g3);
+  } else {
+    const float2 c = ld_twf(twf, idx);
+    const float Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+    const float Ar = __builtin_fmaf(c.x, Rr, -(c.y * Ri));
+    const float Ai = __builtin_fmaf(c.x, Ri, c.y * Rr);
+    const float g0 = __builtin_fmaf(kSf, Lr, Ar), g1 = __builtin_fmaf(kSf, Li, Ai);
+    const float g2 = __builtin_fmaf(kSf, Lr, -Ar), g3 = __builtin_fmaf(-kSf, Li, Ai);
+    const float s0 = kSf * (Lr + Rr), s1 = kSf * (Lr - Rr);
+    const float s2 = kSf * __builtin_fmaf(c.x, Ri, Li), s3 = kSf * (c.y * Ri);
+    lo.x = sp ? s0 : g0;
+    lo.y = sp ? s1 : g1;
+    hi.x = sp ? s2 : g2;
+    hi.y = sp ? s3 : g3;
+  }
+}
+
 // One radix-2 stage on location bit q = q0(P) + I, entirely in registers.
 template <int N, int P, int I, bool FAITH>
-__device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, const DevTables& t) {
+__device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int q = PG::q0(P) + I;
@@ -161,21 +217,20 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, const 
     const int rp = PG::rpart(P, r) & mask;
     const int hi = r | (1 << I);
     if constexpr (P == 0) {
-      if (rp == 0) bfly_special<FAITH>(v[r], v[hi], t.tw, t.twf, mask);
-      else bfly_generic<FAITH>(v[r], v[hi], t.tw, t.twf, mask + rp);
+      if (rp == 0) bfly_special<FAITH>(v[r], v[hi], tw, twf, mask);
+      else bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + rp);
     } else {
-      const int a = la | rp;
-      if (a == 0) bfly_special<FAITH>(v[r], v[hi], t.tw, t.twf, mask);
-      else bfly_generic<FAITH>(v[r], v[hi], t.tw, t.twf, mask + a);
+      if (rp == 0) bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, la == 0);
+      else bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + (la | rp));
     }
   }
 }
 
 template <int N, int P, int I, bool FAITH>
-__device__ __forceinline__ void run_stages(float2 (&v)[Geo<N>::R], int lp, const DevTables& t) {
+__device__ __forceinline__ void run_stages(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf) {
   if constexpr (I < PassGeo<N>::m(P)) {
-    run_stage<N, P, I, FAITH>(v, lp, t);
-    run_stages<N, P, I + 1, FAITH>(v, lp, t);
+    run_stage<N, P, I, FAITH>(v, lp, tw, twf);
+    run_stages<N, P, I + 1, FAITH>(v, lp, tw, twf);
   }
 }
 
@@ -195,16 +250,65 @@ __device__ __forceinline__ void exchange(float2 (&v)[Geo<N>::R], int lp_prev, in
 
 template <int N, int P, bool FAITH>
 __device__ __forceinline__ void run_passes(float2 (&v)[Geo<N>::R], const int (&lp)[Geo<N>::NPASS],
-                                           float2* buf, const DevTables& t) {
+                                           float2* buf, GTw tw, GTwf twf) {
   if constexpr (P < Geo<N>::NPASS) {
     if constexpr (P > 0) exchange<N, P>(v, lp[P - 1], lp[P], buf);
-    run_stages<N, P, 0, FAITH>(v, lp[P], t);
-    run_passes<N, P + 1, FAITH>(v, lp, buf, t);
+    run_stages<N, P, 0, FAITH>(v, lp[P], tw, twf);
+    run_passes<N, P + 1, FAITH>(v, lp, buf, tw, twf);
+  }
+}
+
+// ------------------------------------------------------- DPP wave reductions
+// Cross-lane moves on the VALU (no LDS round trips): quad_perm / row mirrors /
+// row shifts / row broadcasts of gfx9 DPP, applied to both halves of a double.
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROW_MASK, BANK_MASK, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROW_MASK, BANK_MASK, true);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// Sum over the 64 lanes; the result is wave-uniform.
+__device__ __forceinline__ double wave_sum(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror: every lane holds its row's sum
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
+// Inclusive prefix sum over the lanes.
+__device__ __forceinline__ double wave_inclusive_scan(double v) {
+  v += dpp_d<0x111>(v);            // row_shr:1
+  v += dpp_d<0x112>(v);            // row_shr:2
+  v += dpp_d<0x114>(v);            // row_shr:4
+  v += dpp_d<0x118>(v);            // row_shr:8
+  v += dpp_d<0x142, 0xA>(v);       // row_bcast:15 -> rows 1, 3
+  v += dpp_d<0x143, 0xC>(v);       // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// Amplitude of one slot: src/meyda.js:104-114, sqrt(re^2 + im^2) in double, stored to float32.
+template <bool FAITH>
+__device__ __forceinline__ float slot_amp(float re, float im) {
+  if constexpr (FAITH) {
+    const double xr = re, xi = im;
+    return (float)sqrt(__builtin_fma(xr, xr, xi * xi));
+  } else {
+    return sqrtf(__builtin_fmaf(re, re, im * im));
   }
 }
 
 struct FrameRec {
-  double S[5];      // sum_k k^p a_k, p = 0..4
+  double S[5];      // sum_k k^p a_k, p = 0..4 (S[0] = sum a_k)
   double ln2sum;    // sum_k log2 a_k
   double energy;    // sum x^2
   double band[kBark];
@@ -214,274 +318,423 @@ struct FrameRec {
   int roll_m;
 };
 
+// Arguments live in the kernarg segment (constant address space 4: scalar loads).
+typedef const KernelArgs __attribute__((address_space(4))) KArgs;
+
+// Kernel arguments read through an opaque pointer into the kernarg segment: the compiler
+// re-loads fields (scalar loads, K$ hits) after each acquisition point instead of keeping
+// ~40 pointers resident in registers across the whole batch loop.
+__device__ __forceinline__ KArgs* args_ptr() {
+  KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+// Pointers read through args_ptr() are generic; re-type them as global (address space 1)
+// so loads and stores are global_* (vmcnt only), never flat_* (which also ties up lgkmcnt).
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gbl(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 template <typename T>
-__device__ __forceinline__ void put_scalar(const KernelArgs& a, int i, uint64_t f, double v) {
-  if (a.out.scalars[i]) static_cast<T*>(a.out.scalars[i])[f] = (T)v;
+__device__ __forceinline__ void put_scalar(KArgs* a, int i, uint64_t f, double v) {
+  if (a->out.scalars[i]) gbl(static_cast<T*>(a->out.scalars[i]))[f] = (T)v;
+}
+
+template <int N>
+struct Lds {
+  using G = Geo<N>;
+  static constexpr size_t amp_off = 0;
+  static constexpr size_t slot_off = ((size_t)G::FB * G::AS * 4 + 15) / 16 * 16;
+  // phase-2 MFMA partial tiles reuse the slot buffers: [slot][16 rows][16 cols] floats
+  static constexpr size_t slot_bytes = (size_t)4 * G::SLOT_PHYS * 8 > (size_t)kMelSlots * 256 * 4
+                                           ? (size_t)4 * G::SLOT_PHYS * 8 : (size_t)kMelSlots * 256 * 4;
+  static constexpr size_t rec_off = slot_off + slot_bytes;
+  static constexpr size_t bytes = rec_off + (size_t)G::FB * sizeof(FrameRec);
+};
+
+// One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
+template <int N, bool FAITH, bool LITERAL>
+__device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
+                                             int lane, const int (&lp)[Geo<N>::NPASS], const int (&kl)[Geo<N>::R],
+                                             bool dc_lane, float* amp_all, float2* buf, FrameRec* recs) {
+  using G = Geo<N>;
+  using PG = PassGeo<N>;
+  constexpr int L = G::L, R = G::R, CH = G::CH;
+  float* amp = amp_all + fb * G::AS;
+  double* pbuf = reinterpret_cast<double*>(buf);
+
+  // rms.js / energy.js: sum of squares; zcr.js: sign changes of adjacent samples,
+  // `x >= 0` vs `x < 0` (so -0 is non-negative and NaN never counts).
+  float e32 = 0.0f;
+  int z = 0;
+  uint64_t pge = 0, plt = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    e32 = __builtin_fmaf(x[c], x[c], e32);
+    const uint64_t g = __ballot(x[c] >= 0.0f), l = __ballot(x[c] < 0.0f);
+    z += __popcll(((g & (l >> 1)) | (l & (g >> 1))) & 0x7FFFFFFFFFFFFFFFull);
+    if (c > 0) z += (int)((((pge >> 63) & l) | ((plt >> 63) & g)) & 1ull);
+    pge = g;
+    plt = l;
+  }
+  // float32 partial sums are within 1e-6 relative of the double sum; a wave whose
+  // partials leave [2^-100, 2^100] (silence, denormal or huge input) redoes it in double.
+  double e;
+  if (__ballot(!(e32 >= 0x1p-100f && e32 <= 0x1p100f))) {
+    double e64 = 0.0;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) e64 = __builtin_fma((double)x[c], (double)x[c], e64);
+    e = wave_sum(e64);
+  } else {
+    e = wave_sum((double)e32);
+  }
+  if (lane == 0) {
+    recs[fb].energy = e;
+    recs[fb].zcr = z;
+  }
+  if (!ap->need_spectrum) return;
+
+  // src/meyda.js:158-168: windowed[i] = sig[i] * w[i], stored to Float32Array
+  // (the exact double product rounded once == a float32 multiply).
+  {
+    const GF w = gbl(ap->t.window);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) x[c] *= w[c * 64 + lane];
+  }
+  if constexpr (LITERAL) {
+    // The snapshot never transforms per buffer: |w x| is the "spectrum".
+#pragma unroll
+    for (int c = 0; c < R; ++c) amp[c * 64 + lane] = fabsf(x[c]);
+  } else {
+    // Stage 0 (jsfft width 1) at load: slot j = rev(e) pairs x[e] with x[e + N/2].
+    float2 v[R];
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      const int r = rev_bits(c, G::RB);
+      if constexpr (FAITH) {
+        const double xa = x[c], xb = x[c + R];
+        v[r].x = (float)(kS * (xa + xb));
+        v[r].y = (float)(kS * (xa - xb));
+      } else {
+        v[r].x = kSf * (x[c] + x[c + R]);
+        v[r].y = kSf * (x[c] - x[c + R]);
+      }
+    }
+    GTw tw = gbl(ap->t.tw);
+    GTwf twf = gbl(ap->t.twf);
+    run_passes<N, 0, FAITH>(v, lp, buf, tw, twf);
+    const bool want_cplx = ap->out.complex_real != nullptr;
+    // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool dc = (PG::rpart(G::NPASS - 1, r) == 0) && dc_lane;
+      float av = slot_amp<FAITH>(v[r].x, v[r].y);
+      if (dc) av = fabsf(v[r].x);  // slot 0 packs (X[0], X[N/2]), both real
+      amp[kl[r]] = av;
+    }
+    if (want_cplx) {
+      // natural-order half spectrum X[0..N/2] in the slot buffer (freed by the last pass)
+      wave_sync();
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const bool dc = (PG::rpart(G::NPASS - 1, r) == 0) && dc_lane;
+        if (dc) {
+          buf[0] = make_float2(v[r].x, 0.0f);
+          buf[L] = make_float2(v[r].y, 0.0f);
+        } else {
+          buf[kl[r]] = v[r];
+        }
+      }
+      wave_sync();
+      if (valid) {
+        // complexSpectrum.js: the full N-point spectrum, X[N-k] = conj(X[k])
+        auto cr = gbl(ap->out.complex_real) + f * (uint64_t)N;
+        auto ci = gbl(ap->out.complex_imag) + f * (uint64_t)N;
+        for (int i = lane; i < N; i += 64) {
+          const float2 zz = i <= L ? buf[i] : buf[N - i];
+          cr[i] = zz.x;
+          ci[i] = i <= L ? zz.y : -zz.y;
+        }
+      }
+    }
+  }
+  wave_sync();
+
+  if (valid && ap->out.amplitude_spectrum) {
+    auto o = gbl(ap->out.amplitude_spectrum) + f * (uint64_t)L;
+#pragma unroll
+    for (int c = 0; c < R; ++c) o[c * 64 + lane] = amp[c * 64 + lane];
+  }
+  if (valid && ap->out.power_spectrum) {
+    auto o = gbl(ap->out.power_spectrum) + f * (uint64_t)L;
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      const float av = amp[c * 64 + lane];
+      o[c * 64 + lane] = av * av;  // powerSpectrum.js
+    }
+  }
+
+  // Per-frame reductions, lane t owns bins [R t, R t + R).
+  float av[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) av[jj] = amp[R * lane + jj];
+  double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
+  float l2f = 0.0f;
+  double pl[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) {
+    const double ad = av[jj];
+    pl[jj] = T0;
+    T0 += ad;
+    if (jj > 0) {
+      T1 = __builtin_fma((double)jj, ad, T1);
+      T2 = __builtin_fma((double)(jj * jj), ad, T2);
+      T3 = __builtin_fma((double)(jj * jj * jj), ad, T3);
+      T4 = __builtin_fma((double)(jj * jj * jj * jj), ad, T4);
+    }
+    l2f += log2f(av[jj]);
+  }
+  // prefix P(k) = sum_{i<k} a_i: lane-exclusive offset + local prefix
+  const double incl = wave_inclusive_scan(T0);
+  const double excl = dpp_d<0x138>(incl);  // wave_shr:1 (lane 0 reads 0)
+  const double total = readlane_d(incl, 63);
+  // spectralRolloff.js:6-15: the largest m with P(m) <= 0.99 total (P(0) = 0).
+  const double thr = 0.99 * total;
+  int cnt = 0;
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) {
+    const double pk = excl + pl[jj];
+    pbuf[R * lane + jj] = pk;  // the slot buffer is free again (reads above completed)
+    cnt += __popcll(__ballot(pk <= thr));
+  }
+  const int roll_m = (total > thr) ? cnt - 1 : L;
+  const double bb = (double)(R * lane), b2 = bb * bb, b3 = b2 * bb, b4 = b3 * bb;
+  const double S1 = wave_sum(__builtin_fma(bb, T0, T1));
+  const double S2 = wave_sum(T2 + 2.0 * bb * T1 + b2 * T0);
+  const double S3 = wave_sum(T3 + 3.0 * bb * T2 + 3.0 * b2 * T1 + b3 * T0);
+  const double S4 = wave_sum(T4 + 4.0 * bb * T3 + 6.0 * b2 * T2 + 4.0 * b3 * T1 + b4 * T0);
+  const double l2 = wave_sum((double)l2f);
+  wave_sync();
+  FrameRec& rec = recs[fb];
+  if (lane < kBark) {
+    const auto lim = gbl(ap->t.bblim);
+    rec.band[lane] = pbuf[lim[lane + 1]] - pbuf[lim[lane]];
+  }
+  if (lane == 0) {
+    rec.S[0] = total; rec.S[1] = S1; rec.S[2] = S2; rec.S[3] = S3; rec.S[4] = S4;
+    rec.ln2sum = l2;
+    rec.roll_m = roll_m;
+  }
+  wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
+}
+
+// One scalar feature of a frame from its phase-1 record. Formulas as written in the
+// reference extractors; scalars not requested never reach here.
+template <int N>
+__device__ __attribute__((noinline)) double scalar_value(KArgs* q, const FrameRec& rc, int sc) {
+  constexpr int L = N / 2;
+  const double S0 = rc.S[0];
+  switch (sc) {
+    case MGX_ENERGY: return rc.energy;                       // energy.js
+    case MGX_RMS: return sqrt(rc.energy / N);                // rms.js
+    case MGX_ZCR: return (double)rc.zcr;                     // zcr.js
+    case MGX_SPECTRAL_CENTROID: return rc.S[1] / S0;         // spectralCentroid.js -> utils.js:1-11 mu(1)
+    case MGX_SPECTRAL_FLATNESS:                              // spectralFlatness.js: geometric / arithmetic mean
+      return exp(rc.ln2sum * kLn2 / L) * L / S0;
+    case MGX_SPECTRAL_SLOPE: {                               // spectralSlope.js:9-21
+      const double afs = (q->sample_rate / N) * rc.S[1];
+      return (L * afs - q->freq_sum * S0) / (S0 * (q->pow_freq_sum - q->freq_sum * q->freq_sum));
+    }
+    case MGX_SPECTRAL_ROLLOFF: return (double)rc.roll_m * q->nyq_bin;  // spectralRolloff.js:6-15
+    case MGX_SPECTRAL_SPREAD:                                // spectralSpread.js
+    case MGX_SPECTRAL_SKEWNESS:                              // spectralSkewness.js
+    case MGX_SPECTRAL_KURTOSIS: {                            // spectralKurtosis.js (6 mu1 mu2 as written)
+      const double m1 = rc.S[1] / S0, m2 = rc.S[2] / S0;
+      const double var = m2 - m1 * m1, sd = sqrt(var);
+      if (sc == MGX_SPECTRAL_SPREAD) return sd;
+      const double m3 = rc.S[3] / S0;
+      if (sc == MGX_SPECTRAL_SKEWNESS) return (2.0 * m1 * m1 * m1 - 3.0 * m1 * m2 + m3) / (sd * sd * sd);
+      const double m4 = rc.S[4] / S0;
+      return (-3.0 * m1 * m1 * m1 * m1 + 6.0 * m1 * m2 - 4.0 * m1 * m3 + m4) / (sd * sd * sd * sd);
+    }
+    default: {
+      // loudness.js:67-69 total; perceptualSpread.js:7-12 max; perceptualSharpness.js:7-14
+      // (off-by-one spec[i+1] for i < 15, the constant 0.066 e^{0.171 (i+1)} tail after).
+      double total = 0.0, mx = 0.0, sh = 0.0;
+#pragma unroll 1
+      for (int i = 0; i < kBark; ++i) {
+        const double sp = rc.spec[i];
+        total += sp;
+        if (sp > mx) mx = sp;
+        if (i >= 1 && i <= 15) sh += (double)i * sp;
+      }
+      if (sc == MGX_LOUDNESS_TOTAL) return total;
+      if (sc == MGX_PERCEPTUAL_SPREAD) {
+        const double ps = (total - mx) / total;
+        return ps * ps;
+      }
+      sh += q->sharp_tail_sum;
+      return sh * (0.11 / total);
+    }
+  }
 }
 
 template <int N, bool FAITH, bool LITERAL>
 __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
-  constexpr int L = G::L, R = G::R, CH = G::CH, FB = G::FB;
+  using LY = Lds<N>;
+  constexpr int L = G::L, R = G::R, CH = G::CH, FB = G::FB, FPW = G::FPW, AS = G::AS;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* amp_all = reinterpret_cast<float*>(smem);
-  constexpr size_t amp_bytes = ((size_t)FB * G::AMP_STRIDE * 4 + 15) / 16 * 16;
-  float2* slot_all = reinterpret_cast<float2*>(smem + amp_bytes);
-  FrameRec* recs = reinterpret_cast<FrameRec*>(smem + amp_bytes + (size_t)4 * G::SLOT_PHYS * 8);
+  float* amp_all = reinterpret_cast<float*>(smem + LY::amp_off);
+  float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
+  float* part = reinterpret_cast<float*>(smem + LY::slot_off);  // phase-2 alias
+  FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off);
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float2* buf = slot_all + wave * G::SLOT_PHYS;
-  double* pbuf = reinterpret_cast<double*>(buf);
+  KArgs* ap = args_ptr();
+
   int lp[G::NPASS];
 #pragma unroll
   for (int p = 0; p < G::NPASS; ++p) lp[p] = PG::lanepart(p, lane);
+  int kl[R];  // spectrum bin held by each register after the last pass
+  {
+    const auto klist = gbl(ap->t.klist);
+#pragma unroll
+    for (int r = 0; r < R; ++r) kl[r] = klist[lp[G::NPASS - 1] | PG::rpart(G::NPASS - 1, r)];
+  }
+  const bool dc_lane = lp[G::NPASS - 1] == 0;
 
-  const DevTables& t = a.t;
-  const uint64_t nb = (a.num_frames + FB - 1) / FB;
+  const uint64_t nf = ap->num_frames;
+  const uint64_t nb = (nf + FB - 1) / FB;
+  // Register prefetch: the next frame of this wave is loaded while this one is processed.
+  // Loads are unconditional (the frame index is clamped; results of frames past the end
+  // are never stored), so they issue back to back with no branches or waits between them.
+  auto load = [&](float (&xv)[CH], uint64_t b, int j) {
+    uint64_t f = b * FB + j * 4 + wave;
+    f = f < nf ? f : nf - 1;
+    const auto xin = gbl(args_ptr()->frames) + f * (uint64_t)N;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) xv[c] = xin[c * 64 + lane];
+  };
+  float xn[CH];
+  load(xn, blockIdx.x, 0);
+
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const uint64_t f0 = b * FB;
     // ------------------------------------------------------------- phase 1
-    for (int j = 0; j < FB / 4; ++j) {
+    for (int j = 0; j < FPW; ++j) {
       const int fb = j * 4 + wave;
       const uint64_t f = f0 + fb;
-      const bool valid = f < a.num_frames;
-      const float* xin = a.frames + f * (uint64_t)N;
-      float* amp = amp_all + fb * G::AMP_STRIDE;
       float x[CH];
 #pragma unroll
-      for (int c = 0; c < CH; ++c) x[c] = valid ? xin[c * 64 + lane] : 0.0f;
-
-      // rms.js / energy.js: sum of squares (double); zcr.js: sign changes of adjacent
-      // samples, `x >= 0` vs `x < 0` (so -0 is non-negative and NaN never counts).
-      double e = 0.0;
-      int z = 0;
-      uint64_t pge = 0, plt = 0;
-#pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        const double xd = x[c];
-        e = __builtin_fma(xd, xd, e);
-        const uint64_t g = __ballot(x[c] >= 0.0f), l = __ballot(x[c] < 0.0f);
-        z += __popcll(((g & (l >> 1)) | (l & (g >> 1))) & 0x7FFFFFFFFFFFFFFFull);
-        if (c > 0) z += (int)((((pge >> 63) & l) | ((plt >> 63) & g)) & 1ull);
-        pge = g;
-        plt = l;
-      }
-      e = wave_sum(e);
-
-      // src/meyda.js:158-168: windowed[i] = sig[i] * w[i], stored to Float32Array
-      // (the exact double product rounded once == a float32 multiply).
-#pragma unroll
-      for (int c = 0; c < CH; ++c) x[c] *= t.window[c * 64 + lane];
-
-      if (a.need_spectrum) {
-        if constexpr (LITERAL) {
-          // The snapshot never transforms per buffer: |w x| is the "spectrum".
-#pragma unroll
-          for (int c = 0; c < R; ++c) amp[c * 64 + lane] = fabsf(x[c]);
-        } else {
-          // Stage 0 (jsfft width 1) at load: slot j = rev(e) pairs x[e] with x[e + N/2].
-          float2 v[R];
-#pragma unroll
-          for (int c = 0; c < R; ++c) {
-            const int r = rev_bits(c, G::RB);
-            if constexpr (FAITH) {
-              const double xa = x[c], xb = x[c + R];
-              v[r].x = (float)(kS * (xa + xb));
-              v[r].y = (float)(kS * (xa - xb));
-            } else {
-              v[r].x = kSf * (x[c] + x[c + R]);
-              v[r].y = kSf * (x[c] - x[c + R]);
-            }
-          }
-          run_passes<N, 0, FAITH>(v, lp, buf, t);
-
-          // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
-          const int lpl = lp[G::NPASS - 1];
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int rp = PG::rpart(G::NPASS - 1, r);
-            const int loc = lpl | rp;
-            const int k = t.klist[loc];
-            const bool dc = (rp == 0) && (lpl == 0);
-            float av;
-            if constexpr (FAITH) {
-              const double xr = v[r].x, xi = v[r].y;
-              av = (float)sqrt(__builtin_fma(xr, xr, xi * xi));
-            } else {
-              av = sqrtf(__builtin_fmaf(v[r].x, v[r].x, v[r].y * v[r].y));
-            }
-            if (dc) av = fabsf(v[r].x);  // slot 0 packs (X[0], X[N/2]), both real
-            amp[k] = av;
-            if (valid && a.out.complex_real) {
-              float* cr = a.out.complex_real + f * (uint64_t)N;
-              float* ci = a.out.complex_imag + f * (uint64_t)N;
-              if (dc) {
-                cr[0] = v[r].x; ci[0] = 0.0f;
-                cr[L] = v[r].y; ci[L] = 0.0f;
-              } else {
-                cr[k] = v[r].x; ci[k] = v[r].y;
-                cr[N - k] = v[r].x; ci[N - k] = -v[r].y;
-              }
-            }
-          }
-        }
-        wave_sync();
-
-        if (valid && a.out.amplitude_spectrum) {
-#pragma unroll
-          for (int c = 0; c < R; ++c)
-            a.out.amplitude_spectrum[f * (uint64_t)L + c * 64 + lane] = amp[c * 64 + lane];
-        }
-        if (valid && a.out.power_spectrum) {
-#pragma unroll
-          for (int c = 0; c < R; ++c) {
-            const float av = amp[c * 64 + lane];
-            a.out.power_spectrum[f * (uint64_t)L + c * 64 + lane] = av * av;  // powerSpectrum.js
-          }
-        }
-
-        // Per-frame reductions, lane t owns bins [R t, R t + R).
-        double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0, l2 = 0;
-        double pl[R];
-#pragma unroll
-        for (int jj = 0; jj < R; ++jj) {
-          const float av = amp[R * lane + jj];
-          const double ad = av;
-          pl[jj] = T0;
-          T0 += ad;
-          T1 = __builtin_fma((double)jj, ad, T1);
-          T2 = __builtin_fma((double)(jj * jj), ad, T2);
-          T3 = __builtin_fma((double)(jj * jj * jj), ad, T3);
-          T4 = __builtin_fma((double)(jj * jj * jj * jj), ad, T4);
-          l2 += (double)log2f(av);
-        }
-        // exclusive scan of the lane totals -> prefix P(k) = sum_{i<k} a_i
-        double incl = T0;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const double y = __shfl_up(incl, d);
-          if (lane >= d) incl += y;
-        }
-        double excl = __shfl_up(incl, 1);
-        if (lane == 0) excl = 0.0;
-        const double total = __shfl(incl, 63);
-        // spectralRolloff.js:6-15: the largest m with P(m) <= 0.99 total (P(0) = 0).
-        const double thr = 0.99 * total;
-        int cnt = 0;
-        wave_sync();  // the slot buffer is reused as the prefix scratch
-#pragma unroll
-        for (int jj = 0; jj < R; ++jj) {
-          const double pk = excl + pl[jj];
-          pbuf[R * lane + jj] = pk;
-          cnt += __popcll(__ballot(pk <= thr));
-        }
-        const int roll_m = (total > thr) ? cnt - 1 : L;
-        const double bb = (double)(R * lane), b2 = bb * bb, b3 = b2 * bb, b4 = b3 * bb;
-        double S1 = __builtin_fma(bb, T0, T1);
-        double S2 = T2 + 2.0 * bb * T1 + b2 * T0;
-        double S3 = T3 + 3.0 * bb * T2 + 3.0 * b2 * T1 + b3 * T0;
-        double S4 = T4 + 4.0 * bb * T3 + 6.0 * b2 * T2 + 4.0 * b3 * T1 + b4 * T0;
-        S1 = wave_sum(S1);
-        S2 = wave_sum(S2);
-        S3 = wave_sum(S3);
-        S4 = wave_sum(S4);
-        l2 = wave_sum(l2);
-        wave_sync();
-        FrameRec& rec = recs[fb];
-        if (lane < kBark) rec.band[lane] = pbuf[t.bblim[lane + 1]] - pbuf[t.bblim[lane]];
-        if (lane == 0) {
-          rec.S[0] = total; rec.S[1] = S1; rec.S[2] = S2; rec.S[3] = S3; rec.S[4] = S4;
-          rec.ln2sum = l2;
-          rec.roll_m = roll_m;
-        }
-      }
-      if (lane == 0) {
-        recs[fb].energy = e;
-        recs[fb].zcr = z;
-      }
+      for (int c = 0; c < CH; ++c) x[c] = xn[c];
+      if (j + 1 < FPW) load(xn, b, j + 1);
+      else load(xn, b + gridDim.x, 0);
+      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, fb, f, f < nf, lane, lp, kl, dc_lane, amp_all, buf, recs);
     }
-    __syncthreads();
+    lds_barrier();
 
     // ------------------------------------------------------------- phase 2
-    const int tid = threadIdx.x;
-    if (a.need_spectrum && a.need_loudness) {
-      for (int i = tid; i < FB * kBark; i += kThreads) {
-        const int bnd = i / FB, fb = i % FB;
-        const float s = (float)pow(recs[fb].band[bnd], 0.23);  // loudness.js:62
-        recs[fb].spec[bnd] = s;
-        const uint64_t f = f0 + fb;
-        if (f < a.num_frames && a.out.loudness_specific) a.out.loudness_specific[f * kBark + bnd] = s;
-      }
-    }
-    if (a.need_spectrum && a.need_mfcc) {
-      // mfcc.js:53-65: Float32Array accumulator, double products, ascending bins.
-      for (int i = tid; i < FB * a.nfilt; i += kThreads) {
-        const int flt = i / FB, fb = i % FB;
-        const float* amp = amp_all + fb * G::AMP_STRIDE;
-        const int k0 = t.mel_start[flt], cnt = t.mel_cnt[flt];
-        const double* w = t.mel_w + t.mel_off[flt];
-        float acc = 0.0f;
-        for (int q = 0; q < cnt; ++q) {
-          const float av = amp[k0 + q];
-          const float pw = av * av;  // powerSpectrum.js: Math.pow(a, 2) stored to Float32Array
-          acc = (float)((double)acc + w[q] * (double)pw);
-        }
-        recs[fb].lm[flt] = (float)log((double)acc);
-      }
-    }
-    __syncthreads();
-    if (a.need_spectrum && a.need_mfcc) {
-      for (int i = tid; i < FB * a.ncoef; i += kThreads) {
-        const int c = i / FB, fb = i % FB;
-        const uint64_t f = f0 + fb;
-        double v = 0.0;
-        for (int n = 0; n < a.nfilt; ++n) v += (double)t.dct[c + n * a.ncoef] * (double)recs[fb].lm[n];
-        if (f < a.num_frames && a.out.mfcc) a.out.mfcc[f * a.ncoef + c] = (float)(v / a.ncoef);
-      }
-    }
-    if (tid < FB && f0 + tid < a.num_frames) {
-      const FrameRec& rc = recs[tid];
-      const uint64_t f = f0 + tid;
-      double sv[MGX_NUM_SCALARS];
-      sv[MGX_ENERGY] = rc.energy;
-      sv[MGX_RMS] = sqrt(rc.energy / N);
-      sv[MGX_ZCR] = (double)rc.zcr;
-      if (a.need_spectrum) {
-        const double S0 = rc.S[0];
-        const double m1 = rc.S[1] / S0, m2 = rc.S[2] / S0, m3 = rc.S[3] / S0, m4 = rc.S[4] / S0;
-        const double var = m2 - m1 * m1, sd = sqrt(var);
-        sv[MGX_SPECTRAL_CENTROID] = m1;
-        sv[MGX_SPECTRAL_SPREAD] = sd;
-        sv[MGX_SPECTRAL_SKEWNESS] = (2.0 * m1 * m1 * m1 - 3.0 * m1 * m2 + m3) / (sd * sd * sd);
-        sv[MGX_SPECTRAL_KURTOSIS] = (-3.0 * m1 * m1 * m1 * m1 + 6.0 * m1 * m2 - 4.0 * m1 * m3 + m4) / (sd * sd * sd * sd);
-        sv[MGX_SPECTRAL_FLATNESS] = exp(rc.ln2sum * kLn2 / L) * L / S0;
-        const double afs = (a.sample_rate / N) * rc.S[1];
-        sv[MGX_SPECTRAL_SLOPE] = (L * afs - a.freq_sum * S0) / (S0 * (a.pow_freq_sum - a.freq_sum * a.freq_sum));
-        sv[MGX_SPECTRAL_ROLLOFF] = (double)rc.roll_m * a.nyq_bin;
-        if (a.need_loudness) {
-          double total = 0.0, mx = 0.0, sh = 0.0;
-          for (int i = 0; i < kBark; ++i) {
-            total += rc.spec[i];
-            if (rc.spec[i] > mx) mx = rc.spec[i];
+    // Thread ids and the argument pointer are re-derived so that nothing phase 2
+    // needs is hoisted out of the batch loop (it would stay live across the FFT).
+    {
+      KArgs* q = args_ptr();
+      const int t2 = opaque(tid), w2 = opaque(wave), l2 = opaque(lane);
+      if (q->need_spectrum && q->need_mfcc) {
+        // mfcc.js:40-62 as a GEMM on the matrix cores: E[band][frame] = sum_k w[band][k] p[k][frame].
+        // Each wave runs its segments (k-step range of one band tile) of the host schedule;
+        // each segment's 16x16 partial tile goes to its own LDS slot (combined below in a
+        // fixed order, so results are deterministic).
+        const int nseg = gbl(q->t.mel_nseg)[w2];
+        const auto segs = gbl(q->t.mel_seg);
+        const auto wt = gbl(q->t.mel_wt);
+        const int col = l2 & 15, kk = l2 >> 4;
+        const bool colok = col < FB;
+        const float* row = amp_all + (colok ? col : 0) * AS;
+        for (int sidx = 0; sidx < nseg; ++sidx) {
+          const int base = (w2 * kMelMaxSeg + sidx) * 4;
+          // (first k-step index into mel_wt, k-steps, first bin, partial slot)
+          const int s_first = segs[base + 0], s_cnt = segs[base + 1], k_first = segs[base + 2], slot = segs[base + 3];
+          f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+          for (int s = 0; s < s_cnt; ++s) {
+            const int k = k_first + 4 * s + kk;
+            const float av = (colok && k < L) ? row[k] : 0.0f;
+            const float w = wt[(s_first + s) * 64 + l2];
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w, av * av, acc, 0, 0, 0);
           }
-          for (int i = 0; i < kBark; ++i) sh += (i < 15) ? (i + 1) * (double)rc.spec[i + 1] : t.sharp_tail[i];
-          const double ps = (total - mx) / total;
-          sv[MGX_LOUDNESS_TOTAL] = total;
-          sv[MGX_PERCEPTUAL_SPREAD] = ps * ps;
-          sv[MGX_PERCEPTUAL_SHARPNESS] = sh * (0.11 / total);
-        } else {
-          sv[MGX_LOUDNESS_TOTAL] = sv[MGX_PERCEPTUAL_SPREAD] = sv[MGX_PERCEPTUAL_SHARPNESS] = 0.0;
+          float* pt = part + slot * 256;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pt[(kk * 4 + i) * 16 + col] = acc[i];
         }
-      } else {
-        for (int i = MGX_SPECTRAL_CENTROID; i < MGX_NUM_SCALARS; ++i) sv[i] = 0.0;
       }
-      for (int i = 0; i < MGX_NUM_SCALARS; ++i) {
-        if (a.scalar_f64) put_scalar<double>(a, i, f, sv[i]);
-        else put_scalar<float>(a, i, f, sv[i]);
+      if (q->need_spectrum && q->need_loudness) {
+        for (int i = t2; i < FB * kBark; i += kThreads) {
+          const int bnd = i / FB, fb = i % FB;
+          const double sum = recs[fb].band[bnd];
+          // loudness.js:62 Math.pow(sum, 0.23), stored to Float32Array
+          const float s = sum > 0.0 ? (float)exp(0.23 * log(sum)) : (float)pow(sum, 0.23);
+          recs[fb].spec[bnd] = s;
+          const uint64_t f = f0 + fb;
+          if (f < q->num_frames && q->out.loudness_specific) gbl(q->out.loudness_specific)[f * kBark + bnd] = s;
+        }
       }
     }
-    __syncthreads();
+    lds_barrier();
+    {
+      KArgs* q = args_ptr();
+      const int t2 = opaque(tid);
+      if (q->need_spectrum && q->need_mfcc) {
+        // combine the partial tiles (fixed slot order), then mfcc.js:64 log, stored to Float32Array
+        const int nfilt = q->nfilt;
+        const auto tslots = gbl(q->t.mel_tile_slots);
+        for (int i = t2; i < FB * nfilt; i += kThreads) {
+          const int band = i / FB, fb = i % FB, tile = band >> 4, rr = band & 15;
+          float e = 0.0f;
+          for (int u = 0; u < kMelSlotsPerTile; ++u) {
+            const int sl = tslots[tile * kMelSlotsPerTile + u];
+            if (sl >= 0) e += part[sl * 256 + rr * 16 + fb];
+          }
+          recs[fb].lm[band] = (float)log((double)e);
+        }
+      }
+    }
+    lds_barrier();
+    {
+      KArgs* q = args_ptr();
+      const int t2 = opaque(tid);
+      if (q->need_spectrum && q->need_mfcc) {
+        const int nc = q->ncoef, nfilt = q->nfilt;
+        const auto dct = gbl(q->t.dct);
+        for (int i = t2; i < FB * nc; i += kThreads) {
+          const int c = i / FB, fb = i % FB;
+          const uint64_t f = f0 + fb;
+          double v = 0.0;  // mfcc.js:85-93, sequential double sum, /numCoeffs
+          for (int nn = 0; nn < nfilt; ++nn) v += (double)dct[c + nn * nc] * (double)recs[fb].lm[nn];
+          if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(v / nc);
+        }
+      }
+      // scalar features: one thread per (feature, frame)
+      for (int i = t2; i < MGX_NUM_SCALARS * FB; i += kThreads) {
+        const int sc = i / FB, fb = i % FB;
+        const uint64_t f = f0 + fb;
+        void* dst = q->out.scalars[sc];
+        if (f >= q->num_frames || dst == nullptr) continue;
+        const double v = scalar_value<N>(q, recs[fb], sc);
+        if (q->scalar_f64) gbl(static_cast<double*>(dst))[f] = v;
+        else gbl(static_cast<float*>(dst))[f] = (float)v;
+      }
+    }
+    lds_barrier();
   }
 }
 
@@ -505,25 +758,27 @@ __global__ void synth_kernel(float* __restrict__ out, uint64_t count, uint64_t s
   }
 }
 
-template <int N>
-size_t lds_bytes() {
-  using G = Geo<N>;
-  const size_t amp_bytes = ((size_t)G::FB * G::AMP_STRIDE * 4 + 15) / 16 * 16;
-  return amp_bytes + (size_t)4 * G::SLOT_PHYS * 8 + (size_t)G::FB * sizeof(FrameRec);
+template <int N, bool FAITH, bool LITERAL>
+hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
+  const size_t lds = Lds<N>::bytes;
+  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL>), dim3(grid), dim3(kThreads), lds, stream, a);
+  return hipGetLastError();
 }
 
 template <int N, bool FAITH, bool LITERAL>
-hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
-  const size_t lds = lds_bytes<N>();
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&extract_kernel<N, FAITH, LITERAL>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL>), dim3(grid), dim3(kThreads), lds, stream, a);
-  return hipGetLastError();
+int occupancy_n() {
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL>, kThreads,
+                                                   Lds<N>::bytes) != hipSuccess)
+    return 0;
+  return blocks;
+}
+
+template <int N>
+int occupancy_prec(int precision, int mode) {
+  if (mode == MGX_MODE_LITERAL) return occupancy_n<N, true, true>();
+  if (precision == MGX_PRECISION_FAST) return occupancy_n<N, false, false>();
+  return occupancy_n<N, true, false>();
 }
 
 template <int N>
@@ -537,10 +792,10 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
 
 size_t extract_lds_bytes(int n) {
   switch (n) {
-    case 256: return lds_bytes<256>();
-    case 512: return lds_bytes<512>();
-    case 1024: return lds_bytes<1024>();
-    case 2048: return lds_bytes<2048>();
+    case 256: return Lds<256>::bytes;
+    case 512: return Lds<512>::bytes;
+    case 1024: return Lds<1024>::bytes;
+    case 2048: return Lds<2048>::bytes;
     default: return 0;
   }
 }
@@ -551,6 +806,16 @@ int frames_per_batch(int n) {
     case 512: return Geo<512>::FB;
     case 1024: return Geo<1024>::FB;
     case 2048: return Geo<2048>::FB;
+    default: return 0;
+  }
+}
+
+int extract_blocks_per_cu(int n, int precision, int mode) {
+  switch (n) {
+    case 256: return occupancy_prec<256>(precision, mode);
+    case 512: return occupancy_prec<512>(precision, mode);
+    case 1024: return occupancy_prec<1024>(precision, mode);
+    case 2048: return occupancy_prec<2048>(precision, mode);
     default: return 0;
   }
 }

@@ -11,6 +11,13 @@ constexpr int kMaxMel = 64;
 constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
+// MFMA mel filterbank (kernels.hip phase 2): bands in tiles of 16, the k-steps of all
+// tiles split evenly over the 4 waves; every (wave, tile) piece is one segment with its
+// own 16x16 partial tile in LDS.
+constexpr int kMelTiles = kMaxMel / 16;
+constexpr int kMelMaxSeg = kMelTiles;      // segments per wave
+constexpr int kMelSlots = 8;               // partial tiles per workgroup (<= kMelTiles + 3 used)
+constexpr int kMelSlotsPerTile = 4;        // pieces one tile may be cut into
 
 // Device-resident, read-only tables of a plan (one allocation, see plan.cpp).
 struct DevTables {
@@ -19,12 +26,11 @@ struct DevTables {
   const float2* twf;         // same, float32 (MGX_PRECISION_FAST)
   const int* klist;          // N/2: slot location -> spectrum bin
   const int* bblim;          // 25 bark band limits (loudness.js:24-45)
-  const int* mel_start;      // per filter: first bin of its support (clipped to [0, N/2))
-  const int* mel_cnt;        // per filter: support length
-  const int* mel_off;        // per filter: offset into mel_w
-  const double* mel_w;       // filterbank weights on the support (mfcc.js:40-51)
+  const float* mel_wt;       // [k-step][64 lanes] filterbank weights in MFMA A-operand order (mfcc.js:40-51)
+  const int* mel_seg;        // [4 waves][kMelMaxSeg][4]: first k-step, k-steps, first bin, slot
+  const int* mel_nseg;       // [4] segments per wave
+  const int* mel_tile_slots; // [kMelTiles][kMelSlotsPerTile] slots holding each tile's pieces, -1 = none
   const float* dct;          // ncoef * nfilt, dct[c + j*ncoef] (mfcc.js:67-83)
-  const double* sharp_tail;  // 24: 0.066*exp(0.171*(i+1)) for i >= 15 (perceptualSharpness.js:10)
 };
 
 struct KernelArgs {
@@ -36,6 +42,7 @@ struct KernelArgs {
   double freq_sum;       // spectralSlope.js: sum of i*sr/N, i < N/2 (input independent)
   double pow_freq_sum;   // spectralSlope.js: sum of (i*sr/N)^2
   double nyq_bin;        // spectralRolloff.js:4: sr / (2 (N/2 - 1))
+  double sharp_tail_sum; // perceptualSharpness.js:10: sum_{i=15}^{23} 0.066 e^{0.171 (i+1)}
   int nfilt;
   int ncoef;
   int scalar_f64;
@@ -51,5 +58,6 @@ hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t firs
                         hipStream_t stream);
 size_t extract_lds_bytes(int n);
 int frames_per_batch(int n);
+int extract_blocks_per_cu(int n, int precision, int mode);  // resident workgroups per CU
 
 }  // namespace mgx
