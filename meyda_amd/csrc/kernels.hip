@@ -34,11 +34,28 @@ typedef const __attribute__((address_space(1))) double2* GTw;
 typedef const __attribute__((address_space(1))) float2* GTwf;
 typedef const __attribute__((address_space(1))) double* GD;
 typedef const __attribute__((address_space(1))) float* GF;
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr double kS = 0.7071067811865476;  // Math.SQRT1_2 (lib/jsfft/fft.js:10)
 constexpr float kSf = 0.70710677f;
 constexpr double kLn2 = 0.6931471805599453;
+
+// Timing ablations (tools/build_abl.sh): -DMGX_ABL_NO_<PART> drops a phase-2 part.
+#define ABL_ON(part) (!MGX_ABL_NO_##part)
+#ifndef MGX_ABL_NO_LOUD2
+#define MGX_ABL_NO_LOUD2 0
+#endif
+#ifndef MGX_ABL_NO_COMB
+#define MGX_ABL_NO_COMB 0
+#endif
+#ifndef MGX_ABL_NO_DCT
+#define MGX_ABL_NO_DCT 0
+#endif
+#ifndef MGX_ABL_NO_FIN
+#define MGX_ABL_NO_FIN 0
+#endif
+#ifndef MGX_ABL_NO_MELSCAN
+#define MGX_ABL_NO_MELSCAN 0
+#endif
 
 constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v >> 1); }
 constexpr int rev_bits(int x, int bits) {
@@ -219,9 +236,25 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
     if constexpr (P == 0) {
       if (rp == 0) bfly_special<FAITH>(v[r], v[hi], tw, twf, mask);
       else bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + rp);
+#ifndef MGX_ABL_BRANCH
+    } else if (rp == 0) {
+      bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, la == 0);
+#else
+    } else if (rp == 0) {
+      // Block-start on the lanes with la == 0 only: every lane runs the generic
+      // butterfly, then those lanes redo the pair as the block-start one (an exec-masked
+      // branch: cheaper than evaluating and selecting both forms on every lane).
+      const float2 lo0 = v[r], hi0 = v[hi];
+      bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + la);
+      if (la == 0) {
+        float2 a = lo0, b = hi0;
+        bfly_special<FAITH>(a, b, tw, twf, mask);
+        v[r] = a;
+        v[hi] = b;
+      }
+#endif
     } else {
-      if (rp == 0) bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, la == 0);
-      else bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + (la | rp));
+      bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + (la | rp));
     }
   }
 }
@@ -312,8 +345,7 @@ struct FrameRec {
   double ln2sum;    // sum_k log2 a_k
   double energy;    // sum x^2
   double band[kBark];
-  float spec[kBark];
-  float lm[kMaxMel];
+  float lm[kMaxMel];  // mel band energies, then their logs
   int zcr;
   int roll_m;
 };
@@ -352,12 +384,107 @@ struct Lds {
   using G = Geo<N>;
   static constexpr size_t amp_off = 0;
   static constexpr size_t slot_off = ((size_t)G::FB * G::AS * 4 + 15) / 16 * 16;
-  // phase-2 MFMA partial tiles reuse the slot buffers: [slot][16 rows][16 cols] floats
-  static constexpr size_t slot_bytes = (size_t)4 * G::SLOT_PHYS * 8 > (size_t)kMelSlots * 256 * 4
-                                           ? (size_t)4 * G::SLOT_PHYS * 8 : (size_t)kMelSlots * 256 * 4;
+  static constexpr size_t slot_bytes = (size_t)4 * G::SLOT_PHYS * 8;
+  // the mel segment sums (mel_energies) reuse a wave's slot buffer
+  static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2) * 4, "mel scratch must fit");
   static constexpr size_t rec_off = slot_off + slot_bytes;
   static constexpr size_t bytes = rec_off + (size_t)G::FB * sizeof(FrameRec);
 };
+
+// DPP move of one dword (bound_ctrl: lanes without a source read 0).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, true));
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, true);
+}
+
+// One Hillis-Steele step of a segmented inclusive scan over lanes:
+// (f, u, d) <- (f_src | f, f ? (u, d) : (u_src + u, d_src + d)).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ void seg_scan_step(int& f, float& u, float& d) {
+  const float nu = dpp_f<CTRL, ROW_MASK>(u), nd = dpp_f<CTRL, ROW_MASK>(d);
+  const int nf = dpp_i<CTRL, ROW_MASK>(f);
+  if (!f) {
+    u += nu;
+    d += nd;
+  }
+  f |= nf;
+}
+
+// Mel band energies of one frame, mfcc.js:40-62: E_j = sum_k w_jk p_k, p_k = a_k^2 (float32).
+// The triangular filters split the bins into segments m = [b_m, b_{m+1}): every bin
+// belongs to one segment, and band j = (rising half on segment j) + (falling half on
+// segment j+1). So E_j = U_j + D_{j+1} with U_m = sum_{k in m} up(k) p_k and
+// D_m = sum_{k in m} dn(k) p_k: two segmented sums over the bins, computed as in-lane
+// runs plus one segmented scan across the lanes. No cross-segment sums
+// are ever formed, so there is no cancellation; the sums are float32 like the reference's
+// Float32Array accumulation, in a different order.
+template <int N>
+__device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>::R], int lane, float2* buf,
+                                             FrameRec& rec) {
+  constexpr int R = Geo<N>::R;
+  const int nf = ap->nfilt;
+  float* mu = reinterpret_cast<float*>(buf);  // U[0..nf+1], slot nf+1 collects bins of no band
+  float* md = mu + (kMaxMel + 2);
+  wave_sync();  // band-sum reads of the prefix buffer are done
+  for (int i = lane; i < nf + 2; i += 64) {
+    mu[i] = 0.0f;
+    md[i] = 0.0f;
+  }
+  wave_sync();
+  const auto wt = gbl(reinterpret_cast<const float*>(ap->t.mel_wud)) + 2 * R * lane;
+  const auto sg = gbl(ap->t.mel_seg) + R * lane;
+  int prev = dpp_i<0x138>(sg[R - 1]);  // wave_shr:1 -> segment of the previous lane's last bin
+  if (lane == 0) prev = nf + 1;
+  float cu = 0.0f, cd = 0.0f, hu = 0.0f, hd = 0.0f;
+  int hseg = nf + 1, seen = 0;
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) {
+    const int m = sg[jj];
+    const float2 w = make_float2(wt[2 * jj], wt[2 * jj + 1]);  // (rising, falling) weight of this bin
+    const float p = av[jj] * av[jj];  // powerSpectrum.js
+    if (m != prev) {  // bin starts a segment: the open one (ending at the previous bin) closes
+      if (seen) {
+        mu[prev] = cu;
+        md[prev] = cd;
+      } else {
+        hu = cu;
+        hd = cd;
+        hseg = prev;
+      }
+      seen = 1;
+      cu = 0.0f;
+      cd = 0.0f;
+    }
+    cu = __builtin_fmaf(w.x, p, cu);
+    cd = __builtin_fmaf(w.y, p, cd);
+    prev = m;
+  }
+  // segmented inclusive scan of (seen, tail sums) over the lanes
+  int f = seen;
+  float su = cu, sd = cd;
+  seg_scan_step<0x111>(f, su, sd);  // row_shr:1
+  seg_scan_step<0x112>(f, su, sd);  // row_shr:2
+  seg_scan_step<0x114>(f, su, sd);  // row_shr:4
+  seg_scan_step<0x118>(f, su, sd);  // row_shr:8
+  seg_scan_step<0x142, 0xA>(f, su, sd);  // row_bcast:15
+  seg_scan_step<0x143, 0xC>(f, su, sd);  // row_bcast:31
+  const float xu = dpp_f<0x138>(su), xd = dpp_f<0x138>(sd);  // exclusive: carry into this lane
+  if (seen) {
+    mu[hseg] = xu + hu;
+    md[hseg] = xd + hd;
+  }
+  if (lane == 63) {  // the segment still open at the last bin
+    mu[prev] = su;
+    md[prev] = sd;
+  }
+  wave_sync();
+  if (lane < nf) rec.lm[lane] = mu[lane] + md[lane + 1];
+  if (lane + 64 < nf) rec.lm[lane + 64] = mu[lane + 64] + md[lane + 65];
+}
 
 // One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
 template <int N, bool FAITH, bool LITERAL>
@@ -429,7 +556,9 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
     GTw tw = gbl(ap->t.tw);
     GTwf twf = gbl(ap->t.twf);
+#ifndef MGX_ABL_NO_PASSES
     run_passes<N, 0, FAITH>(v, lp, buf, tw, twf);
+#endif
     const bool want_cplx = ap->out.complex_real != nullptr;
     // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
 #pragma unroll
@@ -481,6 +610,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
   }
 
+#ifndef MGX_ABL_NO_REDUCE
   // Per-frame reductions, lane t owns bins [R t, R t + R).
   float av[R];
 #pragma unroll
@@ -532,6 +662,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     rec.ln2sum = l2;
     rec.roll_m = roll_m;
   }
+  if (ABL_ON(MELSCAN) && ap->need_mfcc) mel_energies<N>(ap, av, lane, buf, rec);
+#endif
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
 }
 
@@ -564,25 +696,8 @@ __device__ __attribute__((noinline)) double scalar_value(KArgs* q, const FrameRe
       const double m4 = rc.S[4] / S0;
       return (-3.0 * m1 * m1 * m1 * m1 + 6.0 * m1 * m2 - 4.0 * m1 * m3 + m4) / (sd * sd * sd * sd);
     }
-    default: {
-      // loudness.js:67-69 total; perceptualSpread.js:7-12 max; perceptualSharpness.js:7-14
-      // (off-by-one spec[i+1] for i < 15, the constant 0.066 e^{0.171 (i+1)} tail after).
-      double total = 0.0, mx = 0.0, sh = 0.0;
-#pragma unroll 1
-      for (int i = 0; i < kBark; ++i) {
-        const double sp = rc.spec[i];
-        total += sp;
-        if (sp > mx) mx = sp;
-        if (i >= 1 && i <= 15) sh += (double)i * sp;
-      }
-      if (sc == MGX_LOUDNESS_TOTAL) return total;
-      if (sc == MGX_PERCEPTUAL_SPREAD) {
-        const double ps = (total - mx) / total;
-        return ps * ps;
-      }
-      sh += q->sharp_tail_sum;
-      return sh * (0.11 / total);
-    }
+    default:
+      return 0.0;  // loudness scalars are written in phase 2's loudness step
   }
 }
 
@@ -591,11 +706,10 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   using LY = Lds<N>;
-  constexpr int L = G::L, R = G::R, CH = G::CH, FB = G::FB, FPW = G::FPW, AS = G::AS;
+  constexpr int R = G::R, CH = G::CH, FB = G::FB, FPW = G::FPW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* amp_all = reinterpret_cast<float*>(smem + LY::amp_off);
   float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
-  float* part = reinterpret_cast<float*>(smem + LY::slot_off);  // phase-2 alias
   FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off);
 
   const int lane = threadIdx.x & 63, tid = threadIdx.x;
@@ -644,67 +758,55 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
     }
     lds_barrier();
 
+#ifdef MGX_ABL_NO_PHASE2
+    if (opaque(0)) {
+#endif
     // ------------------------------------------------------------- phase 2
     // Thread ids and the argument pointer are re-derived so that nothing phase 2
     // needs is hoisted out of the batch loop (it would stay live across the FFT).
     {
       KArgs* q = args_ptr();
-      const int t2 = opaque(tid), w2 = opaque(wave), l2 = opaque(lane);
-      if (q->need_spectrum && q->need_mfcc) {
-        // mfcc.js:40-62 as a GEMM on the matrix cores: E[band][frame] = sum_k w[band][k] p[k][frame].
-        // Each wave runs its segments (k-step range of one band tile) of the host schedule;
-        // each segment's 16x16 partial tile goes to its own LDS slot (combined below in a
-        // fixed order, so results are deterministic).
-        const int nseg = gbl(q->t.mel_nseg)[w2];
-        const auto segs = gbl(q->t.mel_seg);
-        const auto wt = gbl(q->t.mel_wt);
-        const int col = l2 & 15, kk = l2 >> 4;
-        const bool colok = col < FB;
-        const float* row = amp_all + (colok ? col : 0) * AS;
-        for (int sidx = 0; sidx < nseg; ++sidx) {
-          const int base = (w2 * kMelMaxSeg + sidx) * 4;
-          // (first k-step index into mel_wt, k-steps, first bin, partial slot)
-          const int s_first = segs[base + 0], s_cnt = segs[base + 1], k_first = segs[base + 2], slot = segs[base + 3];
-          f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-          for (int s = 0; s < s_cnt; ++s) {
-            const int k = k_first + 4 * s + kk;
-            const float av = (colok && k < L) ? row[k] : 0.0f;
-            const float w = wt[(s_first + s) * 64 + l2];
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w, av * av, acc, 0, 0, 0);
-          }
-          float* pt = part + slot * 256;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) pt[(kk * 4 + i) * 16 + col] = acc[i];
-        }
-      }
-      if (q->need_spectrum && q->need_loudness) {
-        for (int i = t2; i < FB * kBark; i += kThreads) {
-          const int bnd = i / FB, fb = i % FB;
-          const double sum = recs[fb].band[bnd];
-          // loudness.js:62 Math.pow(sum, 0.23), stored to Float32Array
-          const float s = sum > 0.0 ? (float)exp(0.23 * log(sum)) : (float)pow(sum, 0.23);
-          recs[fb].spec[bnd] = s;
+      const int t2 = opaque(tid);
+      if (ABL_ON(LOUD2) && q->need_spectrum && q->need_loudness) {
+        // 32 lanes per frame (24 bands + 8 idle), so a frame's reductions stay in two DPP rows.
+        for (int i = t2; i < FB * 32; i += kThreads) {
+          const int fb = i >> 5, bnd = i & 31;
           const uint64_t f = f0 + fb;
-          if (f < q->num_frames && q->out.loudness_specific) gbl(q->out.loudness_specific)[f * kBark + bnd] = s;
-        }
-      }
-    }
-    lds_barrier();
-    {
-      KArgs* q = args_ptr();
-      const int t2 = opaque(tid);
-      if (q->need_spectrum && q->need_mfcc) {
-        // combine the partial tiles (fixed slot order), then mfcc.js:64 log, stored to Float32Array
-        const int nfilt = q->nfilt;
-        const auto tslots = gbl(q->t.mel_tile_slots);
-        for (int i = t2; i < FB * nfilt; i += kThreads) {
-          const int band = i / FB, fb = i % FB, tile = band >> 4, rr = band & 15;
-          float e = 0.0f;
-          for (int u = 0; u < kMelSlotsPerTile; ++u) {
-            const int sl = tslots[tile * kMelSlotsPerTile + u];
-            if (sl >= 0) e += part[sl * 256 + rr * 16 + fb];
+          const bool live = bnd < kBark;
+          const double sum = recs[fb].band[live ? bnd : 0];
+          // loudness.js:62 Math.pow(sum, 0.23), stored to Float32Array
+          float sp = sum > 0.0 ? (float)exp(0.23 * log(sum)) : (float)pow(sum, 0.23);
+          if (!live) sp = 0.0f;
+          if (live && f < q->num_frames && q->out.loudness_specific) gbl(q->out.loudness_specific)[f * kBark + bnd] = sp;
+          // loudness.js:67-69 total; perceptualSpread.js:7-12 max; perceptualSharpness.js:7-14
+          // (off-by-one spec[i+1] for i < 15, then the constant 0.066 e^{0.171 (i+1)} tail).
+          double tot = sp, mx = sp, sh = (bnd >= 1 && bnd <= 15) ? (double)bnd * sp : 0.0;
+          tot += dpp_d<0xB1>(tot); mx = fmax(mx, dpp_d<0xB1>(mx)); sh += dpp_d<0xB1>(sh);
+          tot += dpp_d<0x4E>(tot); mx = fmax(mx, dpp_d<0x4E>(mx)); sh += dpp_d<0x4E>(sh);
+          tot += dpp_d<0x141>(tot); mx = fmax(mx, dpp_d<0x141>(mx)); sh += dpp_d<0x141>(sh);
+          tot += dpp_d<0x140>(tot); mx = fmax(mx, dpp_d<0x140>(mx)); sh += dpp_d<0x140>(sh);
+          // rows 2r and 2r+1 hold one frame: row_bcast:15 adds row 2r's total into row 2r+1
+          tot += dpp_d<0x142, 0xA>(tot); mx = fmax(mx, dpp_d<0x142, 0xA>(mx)); sh += dpp_d<0x142, 0xA>(sh);
+          if (bnd == 31 && f < q->num_frames) {
+            sh += q->sharp_tail_sum;
+            const double ps = (tot - mx) / tot;
+            const double sv[3] = {tot, ps * ps, sh * (0.11 / tot)};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              void* dst = q->out.scalars[MGX_LOUDNESS_TOTAL + k];
+              if (!dst) continue;
+              if (q->scalar_f64) gbl(static_cast<double*>(dst))[f] = sv[k];
+              else gbl(static_cast<float*>(dst))[f] = (float)sv[k];
+            }
           }
-          recs[fb].lm[band] = (float)log((double)e);
+        }
+      }
+      if (ABL_ON(COMB) && q->need_spectrum && q->need_mfcc) {
+        // mfcc.js:64 Math.log of the band energies, stored to Float32Array
+        const int nfilt = q->nfilt;
+        for (int i = t2; i < FB * nfilt; i += kThreads) {
+          const int band = i / FB, fb = i % FB;
+          recs[fb].lm[band] = (float)log((double)recs[fb].lm[band]);
         }
       }
     }
@@ -712,19 +814,33 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
     {
       KArgs* q = args_ptr();
       const int t2 = opaque(tid);
-      if (q->need_spectrum && q->need_mfcc) {
+      if (ABL_ON(DCT) && q->need_spectrum && q->need_mfcc) {
         const int nc = q->ncoef, nfilt = q->nfilt;
         const auto dct = gbl(q->t.dct);
         for (int i = t2; i < FB * nc; i += kThreads) {
           const int c = i / FB, fb = i % FB;
           const uint64_t f = f0 + fb;
+          const float* lm = recs[fb].lm;
           double v = 0.0;  // mfcc.js:85-93, sequential double sum, /numCoeffs
-          for (int nn = 0; nn < nfilt; ++nn) v += (double)dct[c + nn * nc] * (double)recs[fb].lm[nn];
+          for (int n0 = 0; n0 < nfilt; n0 += 8) {
+            float dv[8], lv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {  // clamped, unconditional loads: all issue together
+              const int nn = n0 + u < nfilt ? n0 + u : nfilt - 1;
+              dv[u] = dct[c + nn * nc];
+              lv[u] = lm[nn];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const double t = v + (double)dv[u] * (double)lv[u];
+              v = n0 + u < nfilt ? t : v;
+            }
+          }
           if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(v / nc);
         }
       }
-      // scalar features: one thread per (feature, frame)
-      for (int i = t2; i < MGX_NUM_SCALARS * FB; i += kThreads) {
+      // the other scalar features: one thread per (feature, frame)
+      for (int i = t2; ABL_ON(FIN) && i < MGX_LOUDNESS_TOTAL * FB; i += kThreads) {
         const int sc = i / FB, fb = i % FB;
         const uint64_t f = f0 + fb;
         void* dst = q->out.scalars[sc];
@@ -734,6 +850,9 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
         else gbl(static_cast<float*>(dst))[f] = (float)v;
       }
     }
+#ifdef MGX_ABL_NO_PHASE2
+    }
+#endif
     lds_barrier();
   }
 }

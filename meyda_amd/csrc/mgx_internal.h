@@ -11,14 +11,6 @@ constexpr int kMaxMel = 64;
 constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
-// MFMA mel filterbank (kernels.hip phase 2): bands in tiles of 16, the k-steps of all
-// tiles split evenly over the 4 waves; every (wave, tile) piece is one segment with its
-// own 16x16 partial tile in LDS.
-constexpr int kMelTiles = kMaxMel / 16;
-constexpr int kMelMaxSeg = kMelTiles;      // segments per wave
-constexpr int kMelSlots = 8;               // partial tiles per workgroup (<= kMelTiles + 3 used)
-constexpr int kMelSlotsPerTile = 4;        // pieces one tile may be cut into
-
 // Device-resident, read-only tables of a plan (one allocation, see plan.cpp).
 struct DevTables {
   const float* window;       // N, the selected window (src/meyda.js:116-138)
@@ -26,10 +18,8 @@ struct DevTables {
   const float2* twf;         // same, float32 (MGX_PRECISION_FAST)
   const int* klist;          // N/2: slot location -> spectrum bin
   const int* bblim;          // 25 bark band limits (loudness.js:24-45)
-  const float* mel_wt;       // [k-step][64 lanes] filterbank weights in MFMA A-operand order (mfcc.js:40-51)
-  const int* mel_seg;        // [4 waves][kMelMaxSeg][4]: first k-step, k-steps, first bin, slot
-  const int* mel_nseg;       // [4] segments per wave
-  const int* mel_tile_slots; // [kMelTiles][kMelSlotsPerTile] slots holding each tile's pieces, -1 = none
+  const float2* mel_wud;     // N/2: (rising, falling) filter weight of each bin in its segment (mfcc.js:40-51)
+  const int* mel_seg;        // N/2: segment m of each bin (b_m <= k < b_{m+1}); nfilt + 1 = no band
   const float* dct;          // ncoef * nfilt, dct[c + j*ncoef] (mfcc.js:67-83)
 };
 

@@ -145,62 +145,20 @@ void twiddles(int n, std::vector<double>& tw) {
   }
 }
 
-// MFMA mel schedule (kernels.hip phase 2). Bands are cut into tiles of 16 (the MFMA
-// rows); tile t needs the bins of its bands' supports [bins[16t], bins[min(16t+16, nf)+1]),
-// clipped to the bins the reference sums (j < N/2), in k-steps of 4 bins. The k-steps of
-// all tiles are laid end to end and split into 4 near-equal contiguous runs, one per
-// wave; the run of a wave is cut at tile boundaries into segments, each with its own
-// partial-tile slot. Weights are float32 (within MFCC's tolerance).
-struct MelMfma {
-  std::vector<float> wt;             // [step][64]
-  std::vector<int> seg, nseg, tslots;
-};
-
-double mel_weight(const int32_t* b, int j, int i) {  // mfcc.js:43-50
-  if (i >= b[j] && i < b[j + 1]) return (double)(i - b[j]) / (b[j + 1] - b[j]);
-  if (i >= b[j + 1] && i < b[j + 2]) return (double)(b[j + 2] - i) / (b[j + 2] - b[j + 1]);
-  return 0.0;
-}
-
-void mel_mfma(const int32_t* bins, int nf, int L, MelMfma& m) {
-  const int ntile = (nf + 15) / 16;
-  std::vector<int> t_lo(ntile), t_steps(ntile), t_base(ntile);
-  int total = 0;
-  for (int t = 0; t < ntile; ++t) {
-    const int j0 = 16 * t, j1 = std::min(16 * t + 16, nf);
-    const int lo = std::max(0, std::min(L, (int)bins[j0]));
-    const int hi = std::max(lo, std::min(L, (int)bins[j1 + 1]));
-    t_lo[t] = lo;
-    t_steps[t] = (hi - lo + 3) / 4;
-    t_base[t] = total;
-    total += t_steps[t];
-  }
-  m.wt.assign((size_t)std::max(total, 1) * 64, 0.0f);
-  for (int t = 0; t < ntile; ++t)
-    for (int s = 0; s < t_steps[t]; ++s)
-      for (int l = 0; l < 64; ++l) {
-        const int j = 16 * t + (l & 15), k = t_lo[t] + 4 * s + (l >> 4);
-        if (j < nf && k < L) m.wt[(size_t)(t_base[t] + s) * 64 + l] = (float)mel_weight(bins, j, k);
-      }
-  m.seg.assign(4 * mgx::kMelMaxSeg * 4, 0);
-  m.nseg.assign(4, 0);
-  m.tslots.assign(mgx::kMelTiles * mgx::kMelSlotsPerTile, -1);
-  std::vector<int> tcount(mgx::kMelTiles, 0);
-  int slot = 0;
-  for (int w = 0; w < 4; ++w) {
-    const int g0 = (int)((long)total * w / 4), g1 = (int)((long)total * (w + 1) / 4);
-    for (int t = 0; t < ntile; ++t) {
-      const int a = std::max(g0, t_base[t]), b = std::min(g1, t_base[t] + t_steps[t]);
-      if (a >= b) continue;
-      int* e = &m.seg[(w * mgx::kMelMaxSeg + m.nseg[w]) * 4];
-      e[0] = a;
-      e[1] = b - a;
-      e[2] = t_lo[t] + 4 * (a - t_base[t]);
-      e[3] = slot;
-      m.tslots[t * mgx::kMelSlotsPerTile + tcount[t]++] = slot;
-      ++m.nseg[w];
-      ++slot;
-    }
+// Mel filterbank as per-bin segment tables (kernels.hip mel_energies): bin k lies in
+// segment m with b_m <= k < b_{m+1}, m in [0, nf]; band j rises over segment j and falls
+// over segment j + 1 (mfcc.js:43-50). Bins at or past b_{nf+1} belong to no band.
+void mel_segments(const int32_t* b, int nf, int L, std::vector<float>& wud, std::vector<int>& seg) {
+  wud.assign(2 * (size_t)L, 0.0f);
+  seg.assign(L, nf + 1);
+  for (int k = 0; k < L; ++k) {
+    int m = -1;
+    for (int j = 0; j <= nf; ++j)
+      if (b[j] <= k && k < b[j + 1]) m = j;
+    if (m < 0) continue;
+    seg[k] = m;
+    wud[2 * k] = (float)((double)(k - b[m]) / (b[m + 1] - b[m]));
+    wud[2 * k + 1] = (float)((double)(b[m + 1] - k) / (b[m + 1] - b[m]));
   }
 }
 
@@ -346,8 +304,9 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   for (size_t i = 0; i < tw.size(); ++i) twf[i] = (float)tw[i];
   std::vector<int> kl;
   klist(n, kl);
-  MelMfma mm;
-  mel_mfma(bins.data(), nf, L, mm);
+  std::vector<float> mwud;
+  std::vector<int> mseg;
+  mel_segments(bins.data(), nf, L, mwud, mseg);
 
   auto* p = new mgx_plan();
   p->d = *d;
@@ -367,9 +326,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
                o_twf = carve<float>(off, twf.size()), o_kl = carve<int>(off, L),
-               o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<float>(off, mm.wt.size()),
-               o_seg = carve<int>(off, mm.seg.size()), o_nseg = carve<int>(off, mm.nseg.size()),
-               o_ts = carve<int>(off, mm.tslots.size()), o_dct = carve<float>(off, dct.size());
+               o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<float>(off, mwud.size()),
+               o_seg = carve<int>(off, mseg.size()), o_dct = carve<float>(off, dct.size());
   std::vector<unsigned char> host(off, 0);
   auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) memcpy(host.data() + at, src, bytes); };
   put(o_win, d->window == MGX_WINDOW_HAMMING ? ham.data() : han.data(), n * sizeof(float));
@@ -377,10 +335,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   put(o_twf, twf.data(), twf.size() * sizeof(float));
   put(o_kl, kl.data(), L * sizeof(int));
   put(o_lim, lim, sizeof lim);
-  put(o_mw, mm.wt.data(), mm.wt.size() * sizeof(float));
-  put(o_seg, mm.seg.data(), mm.seg.size() * sizeof(int));
-  put(o_nseg, mm.nseg.data(), mm.nseg.size() * sizeof(int));
-  put(o_ts, mm.tslots.data(), mm.tslots.size() * sizeof(int));
+  put(o_mw, mwud.data(), mwud.size() * sizeof(float));
+  put(o_seg, mseg.data(), mseg.size() * sizeof(int));
   put(o_dct, dct.data(), dct.size() * sizeof(float));
   e = hipMalloc(reinterpret_cast<void**>(&p->dev), off);
   if (e != hipSuccess) { delete p; return hip_fail(e, "hipMalloc(plan tables)"); }
@@ -392,10 +348,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->t.twf = reinterpret_cast<const float2*>(b + o_twf);
   p->t.klist = reinterpret_cast<const int*>(b + o_kl);
   p->t.bblim = reinterpret_cast<const int*>(b + o_lim);
-  p->t.mel_wt = reinterpret_cast<const float*>(b + o_mw);
+  p->t.mel_wud = reinterpret_cast<const float2*>(b + o_mw);
   p->t.mel_seg = reinterpret_cast<const int*>(b + o_seg);
-  p->t.mel_nseg = reinterpret_cast<const int*>(b + o_nseg);
-  p->t.mel_tile_slots = reinterpret_cast<const int*>(b + o_ts);
   p->t.dct = reinterpret_cast<const float*>(b + o_dct);
   *out = p;
   return MGX_OK;
