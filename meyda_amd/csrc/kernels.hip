@@ -72,9 +72,12 @@ struct Geo {
   static constexpr int RB = ilog2c(R);      // register bits
   static constexpr int NPASS = (SB + RB - 1) / RB;
   static constexpr int CH = N / 64;         // 64-sample input chunks per frame
-  static constexpr int FB = N >= 1024 ? 8 : 16;  // frames per workgroup batch (<= 16: one MFMA column tile)
+#ifndef MGX_FB
+  static constexpr int FB = 16;             // frames per workgroup batch (phase 2 works on a batch)
+#else
+  static constexpr int FB = MGX_FB;
+#endif
   static constexpr int FPW = FB / 4;        // frames per wave per batch
-  static constexpr int AS = L + 2;          // amplitude row stride: conflict-free MFMA B-operand reads
   static constexpr int SLOT_PHYS = L + (L >> 4) + 2;
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
@@ -348,7 +351,32 @@ struct FrameRec {
   float lm[kMaxMel];  // mel band energies, then their logs
   int zcr;
   int roll_m;
+  double pad;       // 520 bytes: phase 2 reads across frames hit distinct LDS banks (512 would not)
 };
+
+// Math.pow(x, 0.23) rounded to float32 (loudness.js:62), without the f64 exp/log
+// routines: x = m 2^e with m in [1, 2); log2 m = log2(m_hi) + m_lo / (m_hi ln 2) from the
+// f32 hardware log (m_hi = (float)m); y = 0.23 log2 x in double; 2^y = 2^floor(y) 2^frac(y)
+// with the f32 hardware exp2 on [0, 1). Relative error ~1e-7 (a float32 ulp or two).
+__device__ __forceinline__ float pow023(double x) {
+  if (!(x > 0.0 && x < __builtin_huge_val())) return (float)pow(x, 0.23);  // 0, inf, NaN
+  int e;
+  const double m = 2.0 * frexp(x, &e);  // [1, 2)
+  const float mh = (float)m, ml = (float)(m - (double)mh);
+  const float l2m = __builtin_fmaf(ml, 1.4426950408889634f / mh, __builtin_amdgcn_logf(mh));
+  const double y = 0.23 * ((double)(e - 1) + (double)l2m);
+  const double n = floor(y);
+  return ldexpf(__builtin_amdgcn_exp2f((float)(y - n)), (int)n);
+}
+
+// Math.log(x) of a float32, rounded to float32 (mfcc.js:64): ln x = (e + log2 m) ln 2 with
+// x = m 2^e, m in [1, 2) exact and log2 m from the f32 hardware log; |error| ~4e-8 absolute.
+__device__ __forceinline__ float ln_f32(float x) {
+  if (!(x > 0.0f && x < __builtin_huge_valf())) return (float)log((double)x);  // 0, inf, NaN, < 0
+  int e;
+  const float m = 2.0f * frexpf(x, &e);
+  return (float)(((double)(e - 1) + (double)__builtin_amdgcn_logf(m)) * kLn2);
+}
 
 // Arguments live in the kernarg segment (constant address space 4: scalar loads).
 typedef const KernelArgs __attribute__((address_space(4))) KArgs;
@@ -382,11 +410,11 @@ __device__ __forceinline__ void put_scalar(KArgs* a, int i, uint64_t f, double v
 template <int N>
 struct Lds {
   using G = Geo<N>;
-  static constexpr size_t amp_off = 0;
-  static constexpr size_t slot_off = ((size_t)G::FB * G::AS * 4 + 15) / 16 * 16;
+  // One slot buffer per wave: FFT exchanges, then the frame's amplitude row, its prefix
+  // sums and the mel segment sums (mel_energies) in turn; phase 2 stages the DCT table there.
+  static constexpr size_t slot_off = 0;
   static constexpr size_t slot_bytes = (size_t)4 * G::SLOT_PHYS * 8;
-  // the mel segment sums (mel_energies) reuse a wave's slot buffer
-  static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2) * 4, "mel scratch must fit");
+  static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2 + 64) * 4, "mel scratch must fit");
   static constexpr size_t rec_off = slot_off + slot_bytes;
   static constexpr size_t bytes = rec_off + (size_t)G::FB * sizeof(FrameRec);
 };
@@ -428,7 +456,7 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
   constexpr int R = Geo<N>::R;
   const int nf = ap->nfilt;
   float* mu = reinterpret_cast<float*>(buf);  // U[0..nf+1], slot nf+1 collects bins of no band
-  float* md = mu + (kMaxMel + 2);
+  float* md = mu + (kMaxMel + 2 + 64);
   wave_sync();  // band-sum reads of the prefix buffer are done
   for (int i = lane; i < nf + 2; i += 64) {
     mu[i] = 0.0f;
@@ -436,31 +464,42 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
   }
   wave_sync();
   const auto wt = gbl(reinterpret_cast<const float*>(ap->t.mel_wud)) + 2 * R * lane;
-  const auto sg = gbl(ap->t.mel_seg) + R * lane;
-  int prev = dpp_i<0x138>(sg[R - 1]);  // wave_shr:1 -> segment of the previous lane's last bin
+  // segment ids are bytes, R per lane, read as R/4 dwords (one 16-bit word when R = 2)
+  constexpr int SW = R >= 4 ? R / 4 : 1;
+  uint32_t sgw[SW];
+  if constexpr (R >= 4) {
+    const auto sg = gbl(reinterpret_cast<const uint32_t*>(ap->t.mel_seg)) + SW * lane;
+#pragma unroll
+    for (int i = 0; i < SW; ++i) sgw[i] = sg[i];
+  } else {
+    sgw[0] = gbl(reinterpret_cast<const uint16_t*>(ap->t.mel_seg))[lane];
+  }
+  float2 w[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) w[jj] = make_float2(wt[2 * jj], wt[2 * jj + 1]);  // (rising, falling) weight
+  auto seg_of = [&](int jj) { return (int)((sgw[jj >> 2] >> (8 * (jj & 3))) & 0xFFu); };
+  int prev = dpp_i<0x138>(seg_of(R - 1));  // wave_shr:1 -> segment of the previous lane's last bin
   if (lane == 0) prev = nf + 1;
+  const int dummy = kMaxMel + 2 + lane;  // per-lane sink for the stores a bin does not make
   float cu = 0.0f, cd = 0.0f, hu = 0.0f, hd = 0.0f;
   int hseg = nf + 1, seen = 0;
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) {
-    const int m = sg[jj];
-    const float2 w = make_float2(wt[2 * jj], wt[2 * jj + 1]);  // (rising, falling) weight of this bin
+    const int m = seg_of(jj);
     const float p = av[jj] * av[jj];  // powerSpectrum.js
-    if (m != prev) {  // bin starts a segment: the open one (ending at the previous bin) closes
-      if (seen) {
-        mu[prev] = cu;
-        md[prev] = cd;
-      } else {
-        hu = cu;
-        hd = cd;
-        hseg = prev;
-      }
-      seen = 1;
-      cu = 0.0f;
-      cd = 0.0f;
-    }
-    cu = __builtin_fmaf(w.x, p, cu);
-    cd = __builtin_fmaf(w.y, p, cd);
+    // A bin that starts a segment closes the open one (it ended at the previous bin): an
+    // interior segment is stored now, the lane's first one waits for the carry (head).
+    const bool b = m != prev;
+    const bool st = b && seen, hd_now = b && !seen;
+    const int at = st ? prev : dummy;
+    mu[at] = cu;
+    md[at] = cd;
+    hu = hd_now ? cu : hu;
+    hd = hd_now ? cd : hd;
+    hseg = hd_now ? prev : hseg;
+    seen |= b;
+    cu = __builtin_fmaf(w[jj].x, p, b ? 0.0f : cu);
+    cd = __builtin_fmaf(w[jj].y, p, b ? 0.0f : cd);
     prev = m;
   }
   // segmented inclusive scan of (seen, tail sums) over the lanes
@@ -490,11 +529,11 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
 template <int N, bool FAITH, bool LITERAL>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
                                              int lane, const int (&lp)[Geo<N>::NPASS], const int (&kl)[Geo<N>::R],
-                                             bool dc_lane, float* amp_all, float2* buf, FrameRec* recs) {
+                                             bool dc_lane, float2* buf, FrameRec* recs) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
-  float* amp = amp_all + fb * G::AS;
+  float* amp = reinterpret_cast<float*>(buf);  // the frame's amplitude row, once the FFT is done
   double* pbuf = reinterpret_cast<double*>(buf);
 
   // rms.js / energy.js: sum of squares; zcr.js: sign changes of adjacent samples,
@@ -561,16 +600,16 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #endif
     const bool want_cplx = ap->out.complex_real != nullptr;
     // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
+    float ar[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const bool dc = (PG::rpart(G::NPASS - 1, r) == 0) && dc_lane;
-      float av = slot_amp<FAITH>(v[r].x, v[r].y);
-      if (dc) av = fabsf(v[r].x);  // slot 0 packs (X[0], X[N/2]), both real
-      amp[kl[r]] = av;
+      ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);
+      if (dc) ar[r] = fabsf(v[r].x);  // slot 0 packs (X[0], X[N/2]), both real
     }
+    wave_sync();  // the last exchange's reads are done: the slot buffer is free
     if (want_cplx) {
-      // natural-order half spectrum X[0..N/2] in the slot buffer (freed by the last pass)
-      wave_sync();
+      // natural-order half spectrum X[0..N/2] in the slot buffer
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const bool dc = (PG::rpart(G::NPASS - 1, r) == 0) && dc_lane;
@@ -592,7 +631,10 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
           ci[i] = i <= L ? zz.y : -zz.y;
         }
       }
+      wave_sync();
     }
+#pragma unroll
+    for (int r = 0; r < R; ++r) amp[kl[r]] = ar[r];
   }
   wave_sync();
 
@@ -631,6 +673,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
     l2f += log2f(av[jj]);
   }
+  wave_sync();  // every lane has read the amplitude row: the buffer takes the prefix sums next
   // prefix P(k) = sum_{i<k} a_i: lane-exclusive offset + local prefix
   const double incl = wave_inclusive_scan(T0);
   const double excl = dpp_d<0x138>(incl);  // wave_shr:1 (lane 0 reads 0)
@@ -665,6 +708,28 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   if (ABL_ON(MELSCAN) && ap->need_mfcc) mel_energies<N>(ap, av, lane, buf, rec);
 #endif
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
+}
+
+// mfcc.js:85-93: coefficient c of one frame, sum_n dct[c][n] * lm[n] in double (the order
+// is sequential as written; loads are clamped and unconditional so each group of 8 issues together).
+template <typename P>
+__device__ __forceinline__ double dct_sum(P dct, const float* lm, int c, int nc, int nfilt) {
+  double v = 0.0;
+  for (int n0 = 0; n0 < nfilt; n0 += 8) {
+    float dv[8], lv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int nn = n0 + u < nfilt ? n0 + u : nfilt - 1;
+      dv[u] = dct[c + nn * nc];
+      lv[u] = lm[nn];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double t = v + (double)dv[u] * (double)lv[u];
+      v = n0 + u < nfilt ? t : v;
+    }
+  }
+  return v;
 }
 
 // One scalar feature of a frame from its phase-1 record. Formulas as written in the
@@ -708,7 +773,6 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
   using LY = Lds<N>;
   constexpr int R = G::R, CH = G::CH, FB = G::FB, FPW = G::FPW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* amp_all = reinterpret_cast<float*>(smem + LY::amp_off);
   float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
   FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off);
 
@@ -754,7 +818,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
       for (int c = 0; c < CH; ++c) x[c] = xn[c];
       if (j + 1 < FPW) load(xn, b, j + 1);
       else load(xn, b + gridDim.x, 0);
-      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, fb, f, f < nf, lane, lp, kl, dc_lane, amp_all, buf, recs);
+      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, fb, f, f < nf, lane, lp, kl, dc_lane, buf, recs);
     }
     lds_barrier();
 
@@ -775,7 +839,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
           const bool live = bnd < kBark;
           const double sum = recs[fb].band[live ? bnd : 0];
           // loudness.js:62 Math.pow(sum, 0.23), stored to Float32Array
-          float sp = sum > 0.0 ? (float)exp(0.23 * log(sum)) : (float)pow(sum, 0.23);
+          float sp = pow023(sum);
           if (!live) sp = 0.0f;
           if (live && f < q->num_frames && q->out.loudness_specific) gbl(q->out.loudness_specific)[f * kBark + bnd] = sp;
           // loudness.js:67-69 total; perceptualSpread.js:7-12 max; perceptualSharpness.js:7-14
@@ -802,11 +866,18 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
         }
       }
       if (ABL_ON(COMB) && q->need_spectrum && q->need_mfcc) {
+        // stage the DCT table in the (now idle) slot buffers for the next step
+        const int nt = q->ncoef * q->nfilt;
+        if (nt <= (int)(LY::slot_bytes / 4)) {
+          const auto dct = gbl(q->t.dct);
+          float* dl = reinterpret_cast<float*>(slot_all);
+          for (int i = t2; i < nt; i += kThreads) dl[i] = dct[i];
+        }
         // mfcc.js:64 Math.log of the band energies, stored to Float32Array
         const int nfilt = q->nfilt;
         for (int i = t2; i < FB * nfilt; i += kThreads) {
           const int band = i / FB, fb = i % FB;
-          recs[fb].lm[band] = (float)log((double)recs[fb].lm[band]);
+          recs[fb].lm[band] = ln_f32(recs[fb].lm[band]);
         }
       }
     }
@@ -816,26 +887,12 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
       const int t2 = opaque(tid);
       if (ABL_ON(DCT) && q->need_spectrum && q->need_mfcc) {
         const int nc = q->ncoef, nfilt = q->nfilt;
-        const auto dct = gbl(q->t.dct);
+        const bool staged = nc * nfilt <= (int)(LY::slot_bytes / 4);
         for (int i = t2; i < FB * nc; i += kThreads) {
           const int c = i / FB, fb = i % FB;
           const uint64_t f = f0 + fb;
-          const float* lm = recs[fb].lm;
-          double v = 0.0;  // mfcc.js:85-93, sequential double sum, /numCoeffs
-          for (int n0 = 0; n0 < nfilt; n0 += 8) {
-            float dv[8], lv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {  // clamped, unconditional loads: all issue together
-              const int nn = n0 + u < nfilt ? n0 + u : nfilt - 1;
-              dv[u] = dct[c + nn * nc];
-              lv[u] = lm[nn];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const double t = v + (double)dv[u] * (double)lv[u];
-              v = n0 + u < nfilt ? t : v;
-            }
-          }
+          const double v = staged ? dct_sum(reinterpret_cast<const float*>(slot_all), recs[fb].lm, c, nc, nfilt)
+                                  : dct_sum(gbl(q->t.dct), recs[fb].lm, c, nc, nfilt);
           if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(v / nc);
         }
       }

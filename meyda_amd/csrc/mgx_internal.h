@@ -19,7 +19,7 @@ struct DevTables {
   const int* klist;          // N/2: slot location -> spectrum bin
   const int* bblim;          // 25 bark band limits (loudness.js:24-45)
   const float2* mel_wud;     // N/2: (rising, falling) filter weight of each bin in its segment (mfcc.js:40-51)
-  const int* mel_seg;        // N/2: segment m of each bin (b_m <= k < b_{m+1}); nfilt + 1 = no band
+  const uint8_t* mel_seg;    // N/2: segment m of each bin (b_m <= k < b_{m+1}); nfilt + 1 = no band
   const float* dct;          // ncoef * nfilt, dct[c + j*ncoef] (mfcc.js:67-83)
 };
 

@@ -148,15 +148,15 @@ void twiddles(int n, std::vector<double>& tw) {
 // Mel filterbank as per-bin segment tables (kernels.hip mel_energies): bin k lies in
 // segment m with b_m <= k < b_{m+1}, m in [0, nf]; band j rises over segment j and falls
 // over segment j + 1 (mfcc.js:43-50). Bins at or past b_{nf+1} belong to no band.
-void mel_segments(const int32_t* b, int nf, int L, std::vector<float>& wud, std::vector<int>& seg) {
+void mel_segments(const int32_t* b, int nf, int L, std::vector<float>& wud, std::vector<uint8_t>& seg) {
   wud.assign(2 * (size_t)L, 0.0f);
-  seg.assign(L, nf + 1);
+  seg.assign(L, (uint8_t)(nf + 1));
   for (int k = 0; k < L; ++k) {
     int m = -1;
     for (int j = 0; j <= nf; ++j)
       if (b[j] <= k && k < b[j + 1]) m = j;
     if (m < 0) continue;
-    seg[k] = m;
+    seg[k] = (uint8_t)m;
     wud[2 * k] = (float)((double)(k - b[m]) / (b[m + 1] - b[m]));
     wud[2 * k + 1] = (float)((double)(b[m + 1] - k) / (b[m + 1] - b[m]));
   }
@@ -305,7 +305,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   std::vector<int> kl;
   klist(n, kl);
   std::vector<float> mwud;
-  std::vector<int> mseg;
+  std::vector<uint8_t> mseg;
   mel_segments(bins.data(), nf, L, mwud, mseg);
 
   auto* p = new mgx_plan();
@@ -327,7 +327,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
                o_twf = carve<float>(off, twf.size()), o_kl = carve<int>(off, L),
                o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<float>(off, mwud.size()),
-               o_seg = carve<int>(off, mseg.size()), o_dct = carve<float>(off, dct.size());
+               o_seg = carve<uint8_t>(off, mseg.size()), o_dct = carve<float>(off, dct.size());
   std::vector<unsigned char> host(off, 0);
   auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) memcpy(host.data() + at, src, bytes); };
   put(o_win, d->window == MGX_WINDOW_HAMMING ? ham.data() : han.data(), n * sizeof(float));
@@ -336,7 +336,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   put(o_kl, kl.data(), L * sizeof(int));
   put(o_lim, lim, sizeof lim);
   put(o_mw, mwud.data(), mwud.size() * sizeof(float));
-  put(o_seg, mseg.data(), mseg.size() * sizeof(int));
+  put(o_seg, mseg.data(), mseg.size());
   put(o_dct, dct.data(), dct.size() * sizeof(float));
   e = hipMalloc(reinterpret_cast<void**>(&p->dev), off);
   if (e != hipSuccess) { delete p; return hip_fail(e, "hipMalloc(plan tables)"); }
@@ -349,7 +349,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->t.klist = reinterpret_cast<const int*>(b + o_kl);
   p->t.bblim = reinterpret_cast<const int*>(b + o_lim);
   p->t.mel_wud = reinterpret_cast<const float2*>(b + o_mw);
-  p->t.mel_seg = reinterpret_cast<const int*>(b + o_seg);
+  p->t.mel_seg = reinterpret_cast<const uint8_t*>(b + o_seg);
   p->t.dct = reinterpret_cast<const float*>(b + o_dct);
   *out = p;
   return MGX_OK;
