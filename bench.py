@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--also-fast", action="store_true", help="report the fp32 mode alongside")
+    ap.add_argument("--gather", action="store_true",
+                    help="gather every rank's feature record to rank 0 inside the timed step (RCCL)")
     return ap.parse_args()
 
 
@@ -79,10 +81,12 @@ def capi_seed():
     return meyda_amd.SEED
 
 
-def run_mode(plan, frames, out, steps, warmup, dist, world):
+def run_mode(plan, frames, out, steps, warmup, dist, world, gather=None):
     stream = torch.cuda.current_stream()
     for _ in range(warmup):
         plan.extract_device(frames.data_ptr(), frames.shape[0], out, stream.cuda_stream)
+        if gather:
+            gather()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -93,6 +97,8 @@ def run_mode(plan, frames, out, steps, warmup, dist, world):
         ev[i][0].record(stream)
         plan.extract_device(frames.data_ptr(), frames.shape[0], out, stream.cuda_stream)
         ev[i][1].record(stream)
+        if gather:
+            gather()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -107,14 +113,12 @@ def run_mode(plan, frames, out, steps, warmup, dist, world):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from meyda_amd import dist as mdist
+    rank, local, world = mdist.env_rank_world()
     dist = None
     if world > 1:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        mdist.init("nccl")
         dist = tdist
     else:
         torch.cuda.set_device(0)
@@ -125,7 +129,11 @@ def main():
     plan = capi.Plan(buffer_size=n, precision=args.precision, device=torch.cuda.current_device())
     outs, o = plan.alloc_outputs(F, FEATURES)
     torch.cuda.synchronize()
-    elapsed, kernel_ms = run_mode(plan, frames, o, args.steps, args.warmup, dist, world)
+    gather = None
+    if args.gather and dist:
+        counts = [F] * world
+        gather = lambda: mdist.gather_features(outs, counts, dst=0)  # noqa: E731
+    elapsed, kernel_ms = run_mode(plan, frames, o, args.steps, args.warmup, dist, world, gather)
     fast = None
     if args.also_fast and args.precision != "fast":
         plan_f = capi.Plan(buffer_size=n, precision="fast", device=torch.cuda.current_device())
@@ -158,7 +166,8 @@ def main():
             "data": "synthetic (seeded splitmix64 PCM generated in HBM)",
             "config": {"workload": "C3+C4 all features: %d frames x bufferSize=%d per GPU, float32 outputs" % (F, n),
                        "buffer_size": n, "frames_per_gpu": F, "features": FEATURES,
-                       "precision": args.precision, "parallelism": "frame shards, %d proc" % world},
+                       "precision": args.precision, "parallelism": "frame shards, %d proc" % world,
+                       "gather_to_rank0": bool(gather)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,

@@ -127,7 +127,9 @@ class Meyda {
   get(feature) {
     if (typeof feature === 'object') {
       const names = Array.prototype.slice.call(feature); // null throws, as feature.length does
-      this._compute(names.filter((n) => GPU_FEATURES.has(n) && !this.featureExtractors[n]));
+      try {  // one launch for all built-in features; a failure resurfaces per feature below
+        this._compute(names.filter((n) => GPU_FEATURES.has(n) && !this.featureExtractors[n]));
+      } catch (e) { /* logged per feature, as the reference does */ }
       const results = {};
       for (let x = 0; x < names.length; x++) {
         try {

@@ -1,0 +1,129 @@
+'use strict';
+// GPU checks of the Meyda facade through the N-API addon: per-buffer get() against the
+// reference's own outputs (tests/golden), the batch API against get(), start()/stop()
+// streaming, the hamming window switch and literal mode. Needs an MI355X.
+const assert = require('assert');
+const path = require('path');
+const golden = require('./golden');
+const Meyda = require(path.join(__dirname, '..', '..', 'meyda_amd', 'js', 'meyda.js'));
+
+const ctx = { sampleRate: 44100 };
+const SCALARS = ['rms', 'energy', 'zcr', 'spectralCentroid', 'spectralFlatness', 'spectralSlope',
+  'spectralRolloff', 'spectralSpread', 'spectralSkewness', 'spectralKurtosis'];
+const ALL = SCALARS.concat(['loudness', 'perceptualSpread', 'perceptualSharpness', 'mfcc', 'amplitudeSpectrum']);
+let n = 0;
+const checks = [];
+function check(name, fn) { checks.push([name, fn]); }
+process.on('unhandledRejection', (e) => { console.error(e); process.exit(1); });
+function close(a, b, rtol, atol, what) {
+  if (Number.isNaN(b)) { assert.ok(Number.isNaN(a), what + ': expected NaN, got ' + a); return; }
+  if (!Number.isFinite(b)) { assert.strictEqual(a, b, what); return; }
+  assert.ok(Math.abs(a - b) <= rtol * Math.abs(b) + (atol || 0), what + ': ' + a + ' vs ' + b);
+}
+function frameOf(g, i) { return g.input.subarray(i * g.N, (i + 1) * g.N); }
+function vecClose(a, b, what) {
+  let mx = 0;
+  for (const v of b) if (Number.isFinite(v)) mx = Math.max(mx, Math.abs(v));
+  for (let i = 0; i < b.length; i++) close(a[i], b[i], 1e-5, 1e-5 * mx, what + '[' + i + ']');
+}
+
+const g = golden.load(512);
+const S = g.scalarNames.length;
+
+check('C1: get([rms, spectralCentroid]) on sound1 frame 0', () => {
+  const i = g.labels.indexOf('sound1:0');
+  assert.ok(i >= 0);
+  const m = new Meyda(ctx, null, 512);
+  m.process(frameOf(g, i));
+  const r = m.get(['rms', 'spectralCentroid']);
+  close(r.rms, g.scalars[i * S + 0], 1e-5, 0, 'rms');
+  close(r.spectralCentroid, g.scalars[i * S + 3], 1e-5, 0, 'centroid');
+  m.dispose();
+});
+
+check('per-buffer get() vs reference on noise and wav frames', () => {
+  const m = new Meyda(ctx, null, 512);
+  let frames = 0;
+  for (let i = 0; i < g.F; i++) {
+    const lab = g.labels[i];
+    if (!(lab.startsWith('noise') || lab.startsWith('sound'))) continue;
+    m.process(frameOf(g, i));
+    const r = m.get(ALL);
+    assert.strictEqual(r.zcr, g.scalars[i * S + 2], 'zcr exact');
+    for (const [k, j] of [['rms', 0], ['energy', 1], ['spectralCentroid', 3], ['spectralFlatness', 4],
+      ['spectralRolloff', 6], ['spectralSpread', 7], ['perceptualSpread', 11], ['perceptualSharpness', 12]]) {
+      close(r[k], g.scalars[i * S + j], 1e-5, 0, lab + ' ' + k);
+    }
+    close(r.loudness.total, g.scalars[i * S + 10], 1e-5, 0, lab + ' loudness.total');
+    vecClose(r.loudness.specific, g.loudness_specific.subarray(i * 24, i * 24 + 24), lab + ' specific');
+    vecClose(r.mfcc, g.mfcc.subarray(i * 13, i * 13 + 13), lab + ' mfcc');
+    vecClose(r.amplitudeSpectrum, g.amp.subarray(i * 256, i * 256 + 256), lab + ' amp');
+    assert.ok(r.amplitudeSpectrum instanceof Float32Array && r.mfcc instanceof Float32Array);
+    frames++;
+  }
+  assert.ok(frames > 50);
+  m.dispose();
+});
+
+check('getBatch / getBatchAsync equal per-buffer get()', () => {
+  const m = new Meyda(ctx, null, 512);
+  const F = 40;
+  const x = g.input.subarray(0, F * 512);
+  const b = m.getBatch(ALL, x);
+  for (let i = 0; i < F; i += 7) {
+    m.process(frameOf(g, i));
+    const r = m.get(ALL);
+    for (const k of SCALARS) assert.strictEqual(Meyda.frame(b, k, i, 512), r[k], k);
+    assert.deepStrictEqual(Array.from(Meyda.frame(b, 'mfcc', i, 512)), Array.from(r.mfcc));
+    assert.deepStrictEqual(Meyda.frame(b, 'loudness', i, 512).total, r.loudness.total);
+  }
+  return m.getBatchAsync(ALL, x).then((a) => {
+    for (const k of SCALARS) assert.deepStrictEqual(Array.from(a[k]), Array.from(b[k]), 'async ' + k);
+    m.dispose();
+  });
+});
+
+check('start()/stop() streaming callback', () => {
+  const seen = [];
+  const m = new Meyda(ctx, null, 512, (feat) => seen.push(feat));
+  m.process(frameOf(g, 0));             // not started: no callback
+  m.start(['rms', 'zcr']);
+  for (let i = 0; i < 5; i++) m.process(frameOf(g, i));
+  m.stop();
+  m.process(frameOf(g, 5));             // stopped: no callback
+  assert.strictEqual(seen.length, 5);
+  for (let i = 0; i < 5; i++) {
+    assert.deepStrictEqual(Object.keys(seen[i]).sort(), ['rms', 'zcr']);
+    assert.strictEqual(seen[i].zcr, g.scalars[i * S + 2]);
+  }
+  m.dispose();
+});
+
+check('windowingFunction = hamming', () => {
+  const m = new Meyda(ctx, null, 512);
+  m.windowingFunction = 'hamming';
+  g.hammingFrames = golden.manifest.sizes['512'].hammingFrames;
+  g.hammingFrames.forEach((fi, j) => {
+    m.process(frameOf(g, fi));
+    vecClose(m.get('amplitudeSpectrum'), g.hamming_amp.subarray(j * 256, j * 256 + 256), 'hamming amp');
+  });
+  m.dispose();
+});
+
+check('literal (snapshot) mode is bit-exact', () => {
+  const m = new Meyda(ctx, null, 512, null, { mode: 'literal' });
+  golden.manifest.sizes['512'].literalFrames.forEach((fi, j) => {
+    m.process(frameOf(g, fi));
+    assert.deepStrictEqual(Array.from(m.get('amplitudeSpectrum')), Array.from(g.literal_amp.subarray(j * 256, j * 256 + 256)));
+  });
+  m.dispose();
+});
+
+(async () => {
+  for (const [name, fn] of checks) {
+    await fn();
+    n++;
+    console.log('ok ' + name);
+  }
+  console.log('facade_gpu: ' + n + ' checks passed');
+})().catch((e) => { console.error(e); process.exit(1); });
