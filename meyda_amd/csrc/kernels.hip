@@ -78,7 +78,11 @@ struct Geo {
   static constexpr int FB = MGX_FB;
 #endif
   static constexpr int FPW = FB / 4;        // frames per wave per batch
-  static constexpr int SLOT_PHYS = L + (L >> 4) + 2;
+  // Register budget (VGPRs + AGPRs): 4 waves/SIMD (<= 128) up to N = 1024, where LDS
+  // allows 4 workgroups per CU; 2 waves (<= 256) at N = 2048. Without the bound the
+  // allocator drifts past the threshold (129 VGPRs, or 251 + 32 AGPRs) and occupancy halves.
+  static constexpr int WPE = N <= 1024 ? 4 : 2;
+  static constexpr int SLOT_PHYS = L + (L >> 4) + 2;  // exchange layout (phys); also >= L doubles
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
 
@@ -117,6 +121,7 @@ struct PassGeo {
 
 __device__ __forceinline__ int phys(int loc) { return loc + (loc >> 4); }
 
+
 // Wave-level LDS ordering (no global-memory fence: in-flight prefetch loads stay in flight).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -143,8 +148,9 @@ __device__ __forceinline__ float2 ld_twf(GTwf p, int i) {
 
 // ---------------------------------------------------------------- butterflies
 // Twiddle table of stage q (input blocks of 2^(q+1) samples) at offset 2^q - 1:
-// entry a > 0 holds c = SQRT1_2 * f_k(a) for the slot pair (a, a + 2^q); entry 0
-// holds f_{w/2} unscaled for the block-start pair, whose slots pack (X[0], X[w/2]).
+// entry a holds c = SQRT1_2 * f_k(a) for the slot pair (a, a + 2^q) (entry 0: S f_0 =
+// (S, 0)); after the N/2 - 1 stage entries, entry N/2 - 1 + q holds f_{w/2} unscaled
+// for the block-start pair, whose slots pack (X[0], X[w/2]).
 //
 // Generic pair:      lo <- s L + c R,   hi <- conj(s L - c R)
 // Block-start pair:  exactly jsfft's operations for j = 0 and j = w/2.
@@ -190,32 +196,36 @@ __device__ __forceinline__ void bfly_special(float2& lo, float2& hi, GTw tw, GTw
   }
 }
 
-// A pair that is block-start on some lanes (sp) and generic on the others: both
-// results are formed branch-free and selected, so the wave never diverges.
+// A pair that is block-start on some lanes (sp) and generic on the others: both forms
+// are evaluated and selected, so the wave never diverges. The block-start form keeps
+// jsfft's exact operations (S (L + R), not S L + S R): exact cancellations to 0 (DC /
+// Nyquist of symmetric blocks) must stay 0 for spectralFlatness.
 template <bool FAITH>
-__device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf twf, int idx, bool sp) {
+__device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf twf, int idx, int fidx, bool sp) {
   if constexpr (FAITH) {
     const double2 c = ld_tw(tw, idx);
+    const double2 f = ld_tw(tw, fidx);
     const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
     const double Ar = __builtin_fma(c.x, Rr, -(c.y * Ri));
     const double Ai = __builtin_fma(c.x, Ri, c.y * Rr);
     const double g0 = __builtin_fma(kS, Lr, Ar), g1 = __builtin_fma(kS, Li, Ai);
     const double g2 = __builtin_fma(kS, Lr, -Ar), g3 = __builtin_fma(-kS, Li, Ai);
     const double s0 = kS * (Lr + Rr), s1 = kS * (Lr - Rr);
-    const double s2 = kS * (Li + c.x * Ri), s3 = kS * (c.y * Ri);
+    const double s2 = kS * (Li + f.x * Ri), s3 = kS * (f.y * Ri);
     lo.x = (float)(sp ? s0 : g0);
     lo.y = (float)(sp ? s1 : g1);
     hi.x = (float)(sp ? s2 : g2);
     hi.y = (float)(sp ? s3 : g3);
   } else {
     const float2 c = ld_twf(twf, idx);
+    const float2 f = ld_twf(twf, fidx);
     const float Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
     const float Ar = __builtin_fmaf(c.x, Rr, -(c.y * Ri));
     const float Ai = __builtin_fmaf(c.x, Ri, c.y * Rr);
     const float g0 = __builtin_fmaf(kSf, Lr, Ar), g1 = __builtin_fmaf(kSf, Li, Ai);
     const float g2 = __builtin_fmaf(kSf, Lr, -Ar), g3 = __builtin_fmaf(-kSf, Li, Ai);
     const float s0 = kSf * (Lr + Rr), s1 = kSf * (Lr - Rr);
-    const float s2 = kSf * __builtin_fmaf(c.x, Ri, Li), s3 = kSf * (c.y * Ri);
+    const float s2 = kSf * __builtin_fmaf(f.x, Ri, Li), s3 = kSf * (f.y * Ri);
     lo.x = sp ? s0 : g0;
     lo.y = sp ? s1 : g1;
     hi.x = sp ? s2 : g2;
@@ -230,6 +240,7 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
   using PG = PassGeo<N>;
   constexpr int q = PG::q0(P) + I;
   constexpr int mask = (1 << q) - 1;
+  constexpr int fidx = G::L - 1 + q;  // f_{w/2} of this stage
   const int la = lp & mask;  // 0 in pass 0
 #pragma unroll
   for (int r = 0; r < G::R; ++r) {
@@ -237,11 +248,11 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
     const int rp = PG::rpart(P, r) & mask;
     const int hi = r | (1 << I);
     if constexpr (P == 0) {
-      if (rp == 0) bfly_special<FAITH>(v[r], v[hi], tw, twf, mask);
+      if (rp == 0) bfly_special<FAITH>(v[r], v[hi], tw, twf, fidx);
       else bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + rp);
 #ifndef MGX_ABL_BRANCH
     } else if (rp == 0) {
-      bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, la == 0);
+      bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, fidx, la == 0);
 #else
     } else if (rp == 0) {
       // Block-start on the lanes with la == 0 only: every lane runs the generic
@@ -251,7 +262,7 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
       bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + la);
       if (la == 0) {
         float2 a = lo0, b = hi0;
-        bfly_special<FAITH>(a, b, tw, twf, mask);
+        bfly_special<FAITH>(a, b, tw, twf, fidx);
         v[r] = a;
         v[hi] = b;
       }
@@ -336,8 +347,21 @@ __device__ __forceinline__ double wave_inclusive_scan(double v) {
 template <bool FAITH>
 __device__ __forceinline__ float slot_amp(float re, float im) {
   if constexpr (FAITH) {
+    // s = re^2 + im^2 lies in [2^-298, 2^256) or is 0/inf/NaN, so the library sqrt's
+    // range scaling is not needed: rsq seed + the two-residual refinement (full double
+    // accuracy), then 0/inf/NaN pass through.
     const double xr = re, xi = im;
-    return (float)sqrt(__builtin_fma(xr, xr, xi * xi));
+    const double s = __builtin_fma(xr, xr, xi * xi);
+    const double y = __builtin_amdgcn_rsq(s);
+    double g = s * y, h = 0.5 * y;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, s);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, s);
+    g = __builtin_fma(d, h, g);
+    return (float)((s > 0.0 && s < __builtin_huge_val()) ? g : s);
   } else {
     return sqrtf(__builtin_fmaf(re, re, im * im));
   }
@@ -659,11 +683,9 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   for (int jj = 0; jj < R; ++jj) av[jj] = amp[R * lane + jj];
   double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
   float l2f = 0.0f;
-  double pl[R];
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) {
     const double ad = av[jj];
-    pl[jj] = T0;
     T0 += ad;
     if (jj > 0) {
       T1 = __builtin_fma((double)jj, ad, T1);
@@ -681,11 +703,12 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // spectralRolloff.js:6-15: the largest m with P(m) <= 0.99 total (P(0) = 0).
   const double thr = 0.99 * total;
   int cnt = 0;
+  double pk = excl;  // P(R lane + jj), accumulated again rather than kept (registers)
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) {
-    const double pk = excl + pl[jj];
     pbuf[R * lane + jj] = pk;  // the slot buffer is free again (reads above completed)
     cnt += __popcll(__ballot(pk <= thr));
+    pk += (double)av[jj];
   }
   const int roll_m = (total > thr) ? cnt - 1 : L;
   const double bb = (double)(R * lane), b2 = bb * bb, b3 = b2 * bb, b4 = b3 * bb;
@@ -767,7 +790,7 @@ __device__ __attribute__((noinline)) double scalar_value(KArgs* q, const FrameRe
 }
 
 template <int N, bool FAITH, bool LITERAL>
-__global__ __launch_bounds__(kThreads) void extract_kernel(KernelArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   using LY = Lds<N>;

@@ -115,11 +115,14 @@ void klist(int m, std::vector<int>& k) {
   }
 }
 // lib/jsfft/fft.js:140-165: per stage, f_j by the recurrence from (cos pi/w, sin pi/w).
-// Entry a of stage q (input blocks of w = 2^(q+1) samples): a = 0 holds f_{w/2}
-// (unscaled, for the block-start pair); a > 0 holds SQRT1_2 * f_{k(a)}.
+// Entry a of stage q (input blocks of w = 2^(q+1) samples, offset 2^q - 1) holds
+// SQRT1_2 * f_{k(a)} (a = 0: SQRT1_2 * f_0); entry N/2 - 1 + q holds f_{w/2} unscaled
+// (the block-start pair, kernels.hip bfly_special / bfly_mixed).
 void twiddles(int n, std::vector<double>& tw) {
   const int L = n / 2;
-  tw.assign(2 * (size_t)(L > 1 ? L - 1 : 0), 0.0);
+  int stages = 0;
+  for (int w = 2; w <= L; w <<= 1) ++stages;
+  tw.assign(2 * (size_t)(L - 1 + stages), 0.0);
   size_t off = 0;
   for (int w = 2; w <= L; w <<= 1) {
     const int h = w / 2;
@@ -136,11 +139,14 @@ void twiddles(int n, std::vector<double>& tw) {
     std::vector<int> kl;
     klist(w, kl);
     for (int a = 0; a < h; a++) {
-      const int k = a == 0 ? w / 2 : kl[a];
-      const double sc = a == 0 ? 1.0 : kJsSqrt1_2;
-      tw[2 * (off + a)] = sc * fr[k];
-      tw[2 * (off + a) + 1] = sc * fi[k];
+      const int k = a == 0 ? 0 : kl[a];
+      tw[2 * (off + a)] = kJsSqrt1_2 * fr[k];
+      tw[2 * (off + a) + 1] = kJsSqrt1_2 * fi[k];
     }
+    // f_{w/2} unscaled (block-start pair) after the stage entries
+    const size_t fq = (size_t)(L - 1) + (size_t)(__builtin_ctz((unsigned)w) - 1);
+    tw[2 * fq] = fr[w / 2];
+    tw[2 * fq + 1] = fi[w / 2];
     off += h;
   }
 }
