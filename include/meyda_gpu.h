@@ -18,6 +18,9 @@
  *                         extractor init :208-225)
  *   mgx_extract_device   onaudioprocess + get(features)             src/meyda.js:69-91,244-261
  *   mgx_extract_host     same, for host (pageable) buffers
+ *   mgx_wav_parse,       decodeAudioData + getChannelData(0)        lib/bufferLoader.js:23,
+ *   mgx_pcm_decode_device,                                          src/meyda.js:72
+ *   mgx_extract_host_pcm
  *   mgx_feature_index    the extractor registry by name             src/extractors/index.js:1-20
  *   mgx_feature_info     featureInfo[name].type                     src/feature-info.js:1-65
  *   mgx_last_error       console.error / thrown Error text          src/meyda.js:20-26,249-253
@@ -157,6 +160,49 @@ int mgx_synth_frames_device(float* frames, uint64_t num_frames, uint32_t buffer_
                             uint64_t seed, uint64_t first_frame, void* stream);
 
 int mgx_get_host_tables(const mgx_plan_desc* desc, const mgx_host_tables* out);
+
+/* ---- PCM / WAV ingest ---------------------------------
+ * Replaces the browser's decodeAudioData + getChannelData(0) that feed the
+ * reference (lib/bufferLoader.js:23, index.html:182, src/meyda.js:72): samples of
+ * one channel become float32 exactly as decodeAudioData scales them
+ * (u8: (v-128)/128, s16: v/32768, s24: v/2^23, s32: v/2^31, f32: as stored), and
+ * are cut into non-overlapping buffer_size frames (a trailing partial frame is
+ * dropped, as a ScriptProcessor only delivers full buffers). */
+typedef enum mgx_pcm_format {
+  MGX_PCM_F32 = 0,
+  MGX_PCM_S16 = 1,
+  MGX_PCM_U8 = 2,
+  MGX_PCM_S24 = 3,   /* packed, 3 bytes little-endian */
+  MGX_PCM_S32 = 4
+} mgx_pcm_format;
+
+typedef struct mgx_wav_info {
+  uint32_t struct_size;     /* = sizeof(mgx_wav_info) */
+  uint32_t pcm_format;      /* mgx_pcm_format */
+  uint32_t channels;
+  uint32_t sample_rate;
+  uint32_t bits_per_sample;
+  uint32_t block_align;     /* bytes per sample frame (all channels) */
+  uint64_t data_offset;     /* byte offset of the first sample in the file */
+  uint64_t data_bytes;      /* sample bytes present (the data chunk, clipped to the file) */
+  uint64_t sample_frames;   /* data_bytes / block_align */
+} mgx_wav_info;
+
+/* RIFF/WAVE header walk: 'fmt ' chunk of 16, 18 or 40 (WAVE_FORMAT_EXTENSIBLE)
+ * bytes, PCM (1) or IEEE float (3), chunks in any order, odd sizes padded. Host
+ * only (no device). info->struct_size must be set by the caller. */
+int mgx_wav_parse(const void* bytes, uint64_t num_bytes, mgx_wav_info* info);
+
+/* Device decode: `sample_frames` interleaved frames of `channels` samples at
+ * `pcm` (device memory) -> float32 samples of channel `channel` at `out`. */
+int mgx_pcm_decode_device(const void* pcm, uint64_t sample_frames, uint32_t format, uint32_t channels,
+                          uint32_t channel, float* out, void* stream);
+
+/* Host PCM in, host outputs: floor(sample_frames / buffer_size) buffers of channel
+ * `channel`. The raw PCM (not float32) crosses PCIe and is decoded on the device;
+ * outputs are laid out as for mgx_extract_host. */
+int mgx_extract_host_pcm(mgx_plan* plan, const void* pcm, uint64_t sample_frames, uint32_t format,
+                         uint32_t channels, uint32_t channel, const mgx_outputs* outputs);
 
 int mgx_is_power_of_two(double n);           /* src/utils.js:13-19 */
 int mgx_feature_index(const char* name);     /* -1 if unknown */

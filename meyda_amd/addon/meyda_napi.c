@@ -8,6 +8,10 @@
  *   destroyPlan(plan)
  *   extract(plan, frames, features)      -> { name: TypedArray }   (synchronous)
  *   extractAsync(plan, frames, features) -> Promise<{ name: TypedArray }>  (napi_async_work)
+ *   extractWav(plan, wavBytes, features[, channel]) / extractWavAsync(...)
+ *                                        -> the features of every full buffer of a .wav file;
+ *                                           the raw PCM is decoded on the device
+ *   wavParse(wavBytes)                   -> { pcmFormat, channels, sampleRate, bitsPerSample, ... }
  *   hostTables(opts)                     -> { hanning, hamming, window, barkScale, barkLimits, melBins, dct }
  *   isPowerOfTwo(n), deviceCount(), featureNames(), featureInfo(name), abiVersion()
  * Feature names are the reference extractor names (src/extractors/index.js).
@@ -171,6 +175,10 @@ typedef struct {
   plan_box* box;
   const float* frames;
   uint64_t nframes;
+  /* PCM input (extractWav): interleaved samples, decoded on the device */
+  const unsigned char* pcm;
+  uint64_t pcm_frames;
+  uint32_t pcm_format, pcm_channels, pcm_channel;
   mgx_outputs out;
   void* bufs[NSLOTS];
   size_t bytes[NSLOTS];
@@ -222,6 +230,8 @@ static int parse_features(napi_env env, napi_value feats, job* j) {
   return 1;
 }
 
+static int job_alloc(napi_env env, job* j, napi_value feats);
+
 static int job_prepare(napi_env env, job* j, napi_value frames_v, napi_value feats) {
   bool is_ta = false;
   napi_is_typedarray(env, frames_v, &is_ta);
@@ -246,6 +256,12 @@ static int job_prepare(napi_env env, job* j, napi_value frames_v, napi_value fea
   }
   j->frames = (const float*)data;
   j->nframes = len / n;
+  return job_alloc(env, j, feats);
+}
+
+/* Wanted outputs for j->nframes frames. */
+static int job_alloc(napi_env env, job* j, napi_value feats) {
+  const uint32_t n = j->box->desc.buffer_size;
   if (!parse_features(env, feats, j)) return 0;
   const size_t F = j->nframes, L = n / 2;
   const size_t ss = j->box->desc.scalar_f64 ? 8 : 4;
@@ -274,8 +290,75 @@ static int job_prepare(napi_env env, job* j, napi_value frames_v, napi_value fea
   return 1;
 }
 
+/* wavBytes: a Buffer / Uint8Array / ArrayBuffer holding a whole .wav file. */
+static int bytes_of(napi_env env, napi_value v, const unsigned char** data, size_t* len) {
+  bool is = false;
+  void* d = NULL;
+  napi_is_buffer(env, v, &is);
+  if (is) {
+    napi_get_buffer_info(env, v, &d, len);
+    *data = (const unsigned char*)d;
+    return 1;
+  }
+  napi_is_typedarray(env, v, &is);
+  if (is) {
+    napi_typedarray_type tt;
+    size_t n = 0, off = 0;
+    napi_value ab;
+    napi_get_typedarray_info(env, v, &tt, &n, &d, &ab, &off);
+    if (tt == napi_uint8_array || tt == napi_int8_array || tt == napi_uint8_clamped_array) {
+      *data = (const unsigned char*)d;
+      *len = n;
+      return 1;
+    }
+  }
+  napi_is_arraybuffer(env, v, &is);
+  if (is) {
+    napi_get_arraybuffer_info(env, v, &d, len);
+    *data = (const unsigned char*)d;
+    return 1;
+  }
+  napi_throw_type_error(env, NULL, "expected the bytes of a .wav file (Buffer, Uint8Array or ArrayBuffer)");
+  return 0;
+}
+
+static int job_prepare_wav(napi_env env, job* j, napi_value wav_v, napi_value feats, napi_value chan_v) {
+  const unsigned char* data = NULL;
+  size_t len = 0;
+  if (!bytes_of(env, wav_v, &data, &len)) return 0;
+  mgx_wav_info wi;
+  memset(&wi, 0, sizeof wi);
+  wi.struct_size = sizeof wi;
+  int rc = mgx_wav_parse(data, len, &wi);
+  if (rc) {
+    throw_mgx(env, rc);
+    return 0;
+  }
+  uint32_t ch = 0;
+  if (chan_v) {
+    napi_valuetype t;
+    napi_typeof(env, chan_v, &t);
+    if (t == napi_number) napi_get_value_uint32(env, chan_v, &ch);
+  }
+  if (ch >= wi.channels) {
+    napi_throw_range_error(env, NULL, "channel out of range for this file");
+    return 0;
+  }
+  j->pcm = data + wi.data_offset;
+  j->pcm_frames = wi.sample_frames;
+  j->pcm_format = wi.pcm_format;
+  j->pcm_channels = wi.channels;
+  j->pcm_channel = ch;
+  j->nframes = wi.sample_frames / j->box->desc.buffer_size;
+  return job_alloc(env, j, feats);
+}
+
 static void job_run(job* j) {
-  j->rc = mgx_extract_host(j->box->plan, j->frames, j->nframes, &j->out);
+  if (j->pcm)
+    j->rc = mgx_extract_host_pcm(j->box->plan, j->pcm, j->pcm_frames, j->pcm_format, j->pcm_channels,
+                                 j->pcm_channel, &j->out);
+  else
+    j->rc = mgx_extract_host(j->box->plan, j->frames, j->nframes, &j->out);
   if (j->rc) snprintf(j->err, sizeof j->err, "%s", mgx_last_error());
 }
 
@@ -312,12 +395,12 @@ static napi_value job_result(napi_env env, job* j) {
   return obj;
 }
 
-static napi_value extract_sync(napi_env env, napi_callback_info info) {
-  size_t argc = 3;
-  napi_value argv[3];
+static napi_value extract_common(napi_env env, napi_callback_info info, int wav) {
+  size_t argc = 4;
+  napi_value argv[4];
   CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   if (argc < 3) {
-    napi_throw_type_error(env, NULL, "extract(plan, frames, features)");
+    napi_throw_type_error(env, NULL, wav ? "extractWav(plan, wavBytes, features[, channel])" : "extract(plan, frames, features)");
     return NULL;
   }
   job j;
@@ -328,7 +411,8 @@ static napi_value extract_sync(napi_env env, napi_callback_info info) {
     napi_throw_error(env, NULL, "plan is busy with an async extraction");
     return NULL;
   }
-  if (!job_prepare(env, &j, argv[1], argv[2])) {
+  if (!(wav ? job_prepare_wav(env, &j, argv[1], argv[2], argc > 3 ? argv[3] : NULL)
+            : job_prepare(env, &j, argv[1], argv[2]))) {
     job_free_buffers(&j);
     return NULL;
   }
@@ -344,6 +428,9 @@ static napi_value extract_sync(napi_env env, napi_callback_info info) {
   job_free_buffers(&j);
   return r;
 }
+
+static napi_value extract_sync(napi_env env, napi_callback_info info) { return extract_common(env, info, 0); }
+static napi_value extract_wav_sync(napi_env env, napi_callback_info info) { return extract_common(env, info, 1); }
 
 static void async_execute(napi_env env, void* data) {
   (void)env;
@@ -367,12 +454,13 @@ static void async_complete(napi_env env, napi_status status, void* data) {
   free(j);
 }
 
-static napi_value extract_async(napi_env env, napi_callback_info info) {
-  size_t argc = 3;
-  napi_value argv[3];
+static napi_value extract_async_common(napi_env env, napi_callback_info info, int wav) {
+  size_t argc = 4;
+  napi_value argv[4];
   CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   if (argc < 3) {
-    napi_throw_type_error(env, NULL, "extractAsync(plan, frames, features)");
+    napi_throw_type_error(env, NULL, wav ? "extractWavAsync(plan, wavBytes, features[, channel])"
+                                         : "extractAsync(plan, frames, features)");
     return NULL;
   }
   job* j = (job*)calloc(1, sizeof *j);
@@ -383,7 +471,8 @@ static napi_value extract_async(napi_env env, napi_callback_info info) {
     napi_throw_error(env, NULL, "plan is busy with an async extraction");
     return NULL;
   }
-  if (!job_prepare(env, j, argv[1], argv[2])) {
+  if (!(wav ? job_prepare_wav(env, j, argv[1], argv[2], argc > 3 ? argv[3] : NULL)
+            : job_prepare(env, j, argv[1], argv[2]))) {
     job_free_buffers(j);
     free(j);
     return NULL;
@@ -396,6 +485,37 @@ static napi_value extract_async(napi_env env, napi_callback_info info) {
   j->box->busy = 1;
   CHECK(napi_queue_async_work(env, j->work));
   return promise;
+}
+
+static napi_value extract_async(napi_env env, napi_callback_info info) { return extract_async_common(env, info, 0); }
+static napi_value extract_wav_async(napi_env env, napi_callback_info info) { return extract_async_common(env, info, 1); }
+
+static napi_value wav_parse(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  const unsigned char* data = NULL;
+  size_t len = 0;
+  if (argc < 1 || !bytes_of(env, argv[0], &data, &len)) return NULL;
+  mgx_wav_info wi;
+  memset(&wi, 0, sizeof wi);
+  wi.struct_size = sizeof wi;
+  int rc = mgx_wav_parse(data, len, &wi);
+  if (rc) return throw_mgx(env, rc);
+  static const char* fmts[] = {"f32", "s16", "u8", "s24", "s32"};
+  napi_value obj, v;
+  CHECK(napi_create_object(env, &obj));
+  CHECK(napi_create_string_utf8(env, fmts[wi.pcm_format], NAPI_AUTO_LENGTH, &v));
+  CHECK(napi_set_named_property(env, obj, "pcmFormat", v));
+  const struct { const char* k; double v; } nums[] = {
+      {"channels", wi.channels}, {"sampleRate", wi.sample_rate}, {"bitsPerSample", wi.bits_per_sample},
+      {"blockAlign", wi.block_align}, {"dataOffset", (double)wi.data_offset}, {"dataBytes", (double)wi.data_bytes},
+      {"sampleFrames", (double)wi.sample_frames}};
+  for (size_t i = 0; i < sizeof nums / sizeof nums[0]; ++i) {
+    CHECK(napi_create_double(env, nums[i].v, &v));
+    CHECK(napi_set_named_property(env, obj, nums[i].k, v));
+  }
+  return obj;
 }
 
 /* ---------------------------------------------------------------- host tables */
@@ -488,6 +608,9 @@ static napi_value init(napi_env env, napi_value exports) {
       {"destroyPlan", NULL, destroy_plan, NULL, NULL, NULL, napi_enumerable, NULL},
       {"extract", NULL, extract_sync, NULL, NULL, NULL, napi_enumerable, NULL},
       {"extractAsync", NULL, extract_async, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"extractWav", NULL, extract_wav_sync, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"extractWavAsync", NULL, extract_wav_async, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"wavParse", NULL, wav_parse, NULL, NULL, NULL, napi_enumerable, NULL},
       {"hostTables", NULL, host_tables, NULL, NULL, NULL, napi_enumerable, NULL},
       {"isPowerOfTwo", NULL, is_pow2, NULL, NULL, NULL, napi_enumerable, NULL},
       {"deviceCount", NULL, device_count, NULL, NULL, NULL, napi_enumerable, NULL},

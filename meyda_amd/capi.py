@@ -32,7 +32,9 @@ STATUS = {0: "MGX_OK", -1: "MGX_E_INVALID_ARGUMENT", -2: "MGX_E_NOT_POWER_OF_TWO
 EXPORTS = ["mgx_plan_desc_init", "mgx_plan_create", "mgx_plan_destroy", "mgx_plan_get_desc",
            "mgx_extract_device", "mgx_extract_host", "mgx_synth_frames_device",
            "mgx_get_host_tables", "mgx_is_power_of_two", "mgx_feature_index", "mgx_feature_name",
-           "mgx_feature_info", "mgx_device_count", "mgx_abi_version", "mgx_last_error"]
+           "mgx_feature_info", "mgx_device_count", "mgx_abi_version", "mgx_last_error",
+           "mgx_wav_parse", "mgx_pcm_decode_device", "mgx_extract_host_pcm"]
+PCM_FORMATS = {"f32": 0, "s16": 1, "u8": 2, "s24": 3, "s32": 4}
 
 
 class MgxError(RuntimeError):
@@ -62,6 +64,14 @@ class HostTables(ctypes.Structure):
                 ("hamming", ctypes.c_void_p), ("bark_scale", ctypes.c_void_p),
                 ("bark_limits", ctypes.c_void_p), ("mel_bins", ctypes.c_void_p),
                 ("dct", ctypes.c_void_p)]
+
+
+class WavInfo(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("pcm_format", ctypes.c_uint32),
+                ("channels", ctypes.c_uint32), ("sample_rate", ctypes.c_uint32),
+                ("bits_per_sample", ctypes.c_uint32), ("block_align", ctypes.c_uint32),
+                ("data_offset", ctypes.c_uint64), ("data_bytes", ctypes.c_uint64),
+                ("sample_frames", ctypes.c_uint64)]
 
 
 _lib = None
@@ -100,6 +110,11 @@ def lib():
         L.mgx_feature_info.argtypes = [ctypes.c_int]
         L.mgx_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.mgx_last_error.restype = ctypes.c_char_p
+        L.mgx_wav_parse.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(WavInfo)]
+        L.mgx_pcm_decode_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        L.mgx_extract_host_pcm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(Outputs)]
         _lib = L
     return _lib
 
@@ -225,6 +240,30 @@ class Plan:
         frames = np.ascontiguousarray(frames, dtype=np.float32)
         F, n = frames.shape
         assert n == self.n
+        out, o = self._host_outputs(F, features)
+        check(lib().mgx_extract_host(self._h, frames.ctypes.data, F, ctypes.byref(o)))
+        return out
+
+    def extract_pcm(self, pcm, sample_frames, fmt, channels, channel=0, features=()):
+        """Raw interleaved PCM (bytes / numpy buffer) in host memory -> features of the
+        floor(sample_frames / N) buffers of `channel` (decoded on the device)."""
+        buf = np.frombuffer(pcm, dtype=np.uint8) if not isinstance(pcm, np.ndarray) else pcm.view(np.uint8)
+        buf = np.ascontiguousarray(buf)
+        fmt = PCM_FORMATS[fmt] if isinstance(fmt, str) else fmt
+        F = sample_frames // self.n
+        out, o = self._host_outputs(F, features)
+        check(lib().mgx_extract_host_pcm(self._h, buf.ctypes.data, sample_frames, fmt, channels, channel,
+                                         ctypes.byref(o)))
+        return out
+
+    def extract_wav(self, wav_bytes, features, channel=0):
+        """A whole .wav file (bytes) -> features of its full buffers (channel `channel`)."""
+        info = wav_parse(wav_bytes)
+        data = np.frombuffer(wav_bytes, dtype=np.uint8)[info["data_offset"]:info["data_offset"] + info["data_bytes"]]
+        return self.extract_pcm(data, info["sample_frames"], info["pcm_format"], info["channels"], channel, features)
+
+    def _host_outputs(self, F, features):
+        n = self.n
         L = n // 2
         out, o = {}, Outputs()
         sd = self.scalar_dtype
@@ -253,8 +292,7 @@ class Plan:
                 o.complex_imag = out["complexSpectrum.imag"].ctypes.data
             else:
                 raise ValueError("unknown feature %r" % f)
-        check(lib().mgx_extract_host(self._h, frames.ctypes.data, F, ctypes.byref(o)))
-        return out
+        return out, o
 
 
 ALL_FEATURES = SCALAR_NAMES[:10] + ["loudness", "perceptualSpread", "perceptualSharpness", "mfcc"]
@@ -268,3 +306,22 @@ def synth_frames_device(tensor, seed, first_frame=0, stream=None):
         stream = torch.cuda.current_stream(tensor.device).cuda_stream
     check(lib().mgx_synth_frames_device(ctypes.c_void_p(tensor.data_ptr()), F, n, seed, first_frame,
                                         ctypes.c_void_p(stream)))
+
+
+def wav_parse(data):
+    """RIFF/WAVE header of `data` (bytes): format, channels, rate, data offset/size (no GPU)."""
+    buf = np.frombuffer(data, dtype=np.uint8)
+    info = WavInfo()
+    info.struct_size = ctypes.sizeof(WavInfo)
+    check(lib().mgx_wav_parse(buf.ctypes.data, buf.size, ctypes.byref(info)))
+    return {k: getattr(info, k) for k, _ in WavInfo._fields_ if k != "struct_size"}
+
+
+def pcm_decode_device(pcm_u8, sample_frames, fmt, channels, channel, out, stream=None):
+    """Decode interleaved PCM (a uint8 CUDA tensor) into `out` (float32 CUDA tensor)."""
+    import torch
+    fmt = PCM_FORMATS[fmt] if isinstance(fmt, str) else fmt
+    if stream is None:
+        stream = torch.cuda.current_stream(out.device).cuda_stream
+    check(lib().mgx_pcm_decode_device(ctypes.c_void_p(pcm_u8.data_ptr()), sample_frames, fmt, channels, channel,
+                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))

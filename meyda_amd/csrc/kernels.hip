@@ -957,6 +957,28 @@ __global__ void synth_kernel(float* __restrict__ out, uint64_t count, uint64_t s
   }
 }
 
+// PCM -> float32 of one channel, decodeAudioData's scaling (include/meyda_gpu.h).
+__global__ void pcm_decode_kernel(const unsigned char* __restrict__ pcm, uint64_t count, uint32_t format,
+                                  uint32_t stride, uint32_t offset, float* __restrict__ out) {
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += step) {
+    const unsigned char* b = pcm + i * stride + offset;
+    float v;
+    switch (format) {
+      case MGX_PCM_S16: v = (float)*reinterpret_cast<const int16_t*>(b) * (1.0f / 32768.0f); break;
+      case MGX_PCM_U8: v = (float)((int)b[0] - 128) * (1.0f / 128.0f); break;
+      case MGX_PCM_S24: {
+        const int32_t u = (int32_t)((uint32_t)b[0] << 8 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 24) >> 8;
+        v = (float)u * (1.0f / 8388608.0f);
+        break;
+      }
+      case MGX_PCM_S32: v = (float)((double)*reinterpret_cast<const int32_t*>(b) * (1.0 / 2147483648.0)); break;
+      default: v = *reinterpret_cast<const float*>(b); break;
+    }
+    out[i] = v;
+  }
+}
+
 template <int N, bool FAITH, bool LITERAL>
 hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
   const size_t lds = Lds<N>::bytes;
@@ -1028,6 +1050,16 @@ hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, i
     case 2048: return launch_prec<2048>(precision, mode, a, grid, stream);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_pcm_decode(const void* pcm, uint64_t count, uint32_t format, uint32_t channels,
+                             uint32_t channel, float* out, hipStream_t stream) {
+  const uint32_t bps = format == MGX_PCM_S16 ? 2 : format == MGX_PCM_U8 ? 1 : format == MGX_PCM_S24 ? 3 : 4;
+  uint64_t blocks = (count + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(pcm_decode_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     static_cast<const unsigned char*>(pcm), count, format, bps * channels, bps * channel, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t first_index,

@@ -46,6 +46,8 @@ hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, i
                           hipStream_t stream);
 hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t first_index,
                         hipStream_t stream);
+hipError_t launch_pcm_decode(const void* pcm, uint64_t count, uint32_t format, uint32_t channels,
+                             uint32_t channel, float* out, hipStream_t stream);
 size_t extract_lds_bytes(int n);
 int frames_per_batch(int n);
 int extract_blocks_per_cu(int n, int precision, int mode);  // resident workgroups per CU

@@ -36,6 +36,7 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(code, "%s: %s", what, hipGetErrorString(e));
 }
 
+const uint64_t kHostChunk = 65536;              // frames per host-staging chunk
 const double kJsPi = 3.141592653589793;        // Math.PI
 const double kJsSqrt1_2 = 0.7071067811865476;  // Math.SQRT1_2
 
@@ -209,6 +210,8 @@ struct mgx_plan {
   unsigned char* s_out = nullptr;
   size_t s_out_bytes = 0;
   uint64_t s_chunk = 0;
+  unsigned char* s_pcm = nullptr;   // staging for mgx_extract_host_pcm
+  uint64_t s_pcm_bytes = 0;
 };
 
 extern "C" {
@@ -367,6 +370,7 @@ int mgx_plan_destroy(mgx_plan* p) {
   if (p->dev) (void)hipFree(p->dev);
   if (p->s_frames) (void)hipFree(p->s_frames);
   if (p->s_out) (void)hipFree(p->s_out);
+  if (p->s_pcm) (void)hipFree(p->s_pcm);
   delete p;
   return MGX_OK;
 }
@@ -412,10 +416,15 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   return MGX_OK;
 }
 
-int mgx_extract_host(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o) {
-  if (!p || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL plan or outputs");
-  if (nframes == 0) return MGX_OK;
-  if (!frames) return fail(MGX_E_INVALID_ARGUMENT, "frames is NULL");
+}  // extern "C"
+
+namespace {
+
+// Host batches: stage `nframes` frames through plan-owned device buffers in chunks.
+// `fill(f0, cnt)` puts frames [f0, f0 + cnt) into p->s_frames; outputs come back to the
+// host arrays of `o` (laid out over all nframes).
+template <typename Fill>
+int extract_host_chunked(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill fill) {
   const int n = p->n, L = p->L;
   const size_t ss = p->d.scalar_f64 ? 8 : 4;
   const size_t nb = mgx::kBark, nc = p->d.num_mfcc_coeffs;
@@ -424,7 +433,7 @@ int mgx_extract_host(mgx_plan* p, const float* frames, uint64_t nframes, const m
   for (int i = 0; i < MGX_NUM_SCALARS; ++i) per += o->scalars[i] ? ss : 0;
   per += (o->loudness_specific ? nb * 4 : 0) + (o->mfcc ? nc * 4 : 0) + (o->amplitude_spectrum ? L * 4 : 0) +
          (o->power_spectrum ? L * 4 : 0) + (o->complex_real ? 2 * (size_t)n * 4 : 0);
-  const uint64_t chunk = std::min<uint64_t>(nframes, 65536);
+  const uint64_t chunk = std::min<uint64_t>(nframes, kHostChunk);
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if (p->s_chunk < chunk || p->s_out_bytes < per * chunk + 4096) {
@@ -444,8 +453,8 @@ int mgx_extract_host(mgx_plan* p, const float* frames, uint64_t nframes, const m
   }
   for (uint64_t f0 = 0; f0 < nframes; f0 += chunk) {
     const uint64_t cnt = std::min<uint64_t>(chunk, nframes - f0);
-    e = hipMemcpy(p->s_frames, frames + f0 * n, cnt * n * sizeof(float), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(frames)");
+    int rc = fill(f0, cnt);
+    if (rc) return rc;
     mgx_outputs d{};
     size_t off = 0;
     auto take = [&](size_t bytes) { unsigned char* q = p->s_out + off; off += (bytes + 255) / 256 * 256; return q; };
@@ -456,7 +465,7 @@ int mgx_extract_host(mgx_plan* p, const float* frames, uint64_t nframes, const m
     d.power_spectrum = o->power_spectrum ? reinterpret_cast<float*>(take(cnt * L * 4)) : nullptr;
     d.complex_real = o->complex_real ? reinterpret_cast<float*>(take(cnt * n * 4)) : nullptr;
     d.complex_imag = o->complex_imag ? reinterpret_cast<float*>(take(cnt * n * 4)) : nullptr;
-    int rc = mgx_extract_device(p, p->s_frames, cnt, &d, nullptr);
+    rc = mgx_extract_device(p, p->s_frames, cnt, &d, nullptr);
     if (rc) return rc;
     auto back = [&](void* host, const void* dev, size_t bytes) {
       return host ? hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost) : hipSuccess;
@@ -472,6 +481,135 @@ int mgx_extract_host(mgx_plan* p, const float* frames, uint64_t nframes, const m
     if (e != hipSuccess) return hip_fail(e, "hipMemcpy(outputs)");
   }
   return MGX_OK;
+}
+
+uint32_t pcm_bytes(uint32_t format) {
+  switch (format) {
+    case MGX_PCM_F32: return 4;
+    case MGX_PCM_S16: return 2;
+    case MGX_PCM_U8: return 1;
+    case MGX_PCM_S24: return 3;
+    case MGX_PCM_S32: return 4;
+    default: return 0;
+  }
+}
+
+uint16_t rd16(const unsigned char* b) { return (uint16_t)(b[0] | (b[1] << 8)); }
+uint32_t rd32(const unsigned char* b) { return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24); }
+
+}  // namespace
+
+extern "C" {
+
+int mgx_extract_host(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o) {
+  if (!p || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL plan or outputs");
+  if (nframes == 0) return MGX_OK;
+  if (!frames) return fail(MGX_E_INVALID_ARGUMENT, "frames is NULL");
+  if ((o->complex_real == nullptr) != (o->complex_imag == nullptr))
+    return fail(MGX_E_INVALID_ARGUMENT, "complex_real and complex_imag must be given together");
+  const int n = p->n;
+  return extract_host_chunked(p, nframes, o, [&](uint64_t f0, uint64_t cnt) {
+    hipError_t e = hipMemcpy(p->s_frames, frames + f0 * n, cnt * n * sizeof(float), hipMemcpyHostToDevice);
+    return e == hipSuccess ? MGX_OK : hip_fail(e, "hipMemcpy(frames)");
+  });
+}
+
+int mgx_wav_parse(const void* bytes, uint64_t len, mgx_wav_info* info) {
+  if (!bytes || !info) return fail(MGX_E_INVALID_ARGUMENT, "NULL argument");
+  if (info->struct_size != sizeof(mgx_wav_info))
+    return fail(MGX_E_INVALID_ARGUMENT, "mgx_wav_info.struct_size is %u, expected %zu", info->struct_size, sizeof(mgx_wav_info));
+  const unsigned char* b = static_cast<const unsigned char*>(bytes);
+  if (len < 12 || memcmp(b, "RIFF", 4) != 0 || memcmp(b + 8, "WAVE", 4) != 0)
+    return fail(MGX_E_INVALID_ARGUMENT, "not a RIFF/WAVE file");
+  bool have_fmt = false;
+  uint16_t tag = 0, channels = 0, bits = 0, align = 0;
+  uint32_t rate = 0;
+  uint64_t off = 12;
+  while (off + 8 <= len) {
+    const unsigned char* c = b + off;
+    const uint64_t size = rd32(c + 4);
+    if (memcmp(c, "fmt ", 4) == 0) {
+      if (size < 16 || off + 8 + 16 > len) return fail(MGX_E_INVALID_ARGUMENT, "truncated fmt chunk");
+      tag = rd16(c + 8);
+      channels = rd16(c + 10);
+      rate = rd32(c + 12);
+      align = rd16(c + 20);
+      bits = rd16(c + 22);
+      if (tag == 0xFFFE) {  // WAVE_FORMAT_EXTENSIBLE: the subformat GUID starts with the real tag
+        if (size < 40 || off + 8 + 26 > len) return fail(MGX_E_INVALID_ARGUMENT, "truncated WAVE_FORMAT_EXTENSIBLE fmt chunk");
+        tag = rd16(c + 8 + 24);
+      }
+      have_fmt = true;
+    } else if (memcmp(c, "data", 4) == 0) {
+      if (!have_fmt) return fail(MGX_E_INVALID_ARGUMENT, "data chunk before fmt chunk");
+      uint32_t fmt = 0xFFFFFFFFu;
+      if (tag == 1 && bits == 8) fmt = MGX_PCM_U8;
+      else if (tag == 1 && bits == 16) fmt = MGX_PCM_S16;
+      else if (tag == 1 && bits == 24) fmt = MGX_PCM_S24;
+      else if (tag == 1 && bits == 32) fmt = MGX_PCM_S32;
+      else if (tag == 3 && bits == 32) fmt = MGX_PCM_F32;
+      if (fmt == 0xFFFFFFFFu) return fail(MGX_E_UNSUPPORTED, "unsupported WAV encoding (format tag %u, %u bits)", tag, bits);
+      if (channels == 0) return fail(MGX_E_INVALID_ARGUMENT, "WAV with 0 channels");
+      if (align != channels * pcm_bytes(fmt))
+        return fail(MGX_E_INVALID_ARGUMENT, "block_align %u does not match %u channels x %u bytes", align, channels, pcm_bytes(fmt));
+      const uint64_t avail = len - (off + 8);
+      const uint64_t data = std::min<uint64_t>(size, avail);
+      info->pcm_format = fmt;
+      info->channels = channels;
+      info->sample_rate = rate;
+      info->bits_per_sample = bits;
+      info->block_align = align;
+      info->data_offset = off + 8;
+      info->data_bytes = data / align * align;
+      info->sample_frames = data / align;
+      return MGX_OK;
+    }
+    off += 8 + size + (size & 1);
+  }
+  return fail(MGX_E_INVALID_ARGUMENT, have_fmt ? "no data chunk" : "no fmt chunk");
+}
+
+int mgx_pcm_decode_device(const void* pcm, uint64_t sample_frames, uint32_t format, uint32_t channels,
+                          uint32_t channel, float* out, void* stream) {
+  if (sample_frames == 0) return MGX_OK;
+  if (!pcm || !out) return fail(MGX_E_INVALID_ARGUMENT, "NULL pointer");
+  if (!pcm_bytes(format)) return fail(MGX_E_INVALID_ARGUMENT, "unknown PCM format %u", format);
+  if (channels == 0 || channel >= channels) return fail(MGX_E_INVALID_ARGUMENT, "channel %u of %u", channel, channels);
+  hipError_t e = mgx::launch_pcm_decode(pcm, sample_frames, format, channels, channel, out, (hipStream_t)stream);
+  return e == hipSuccess ? MGX_OK : hip_fail(e, "PCM decode launch");
+}
+
+int mgx_extract_host_pcm(mgx_plan* p, const void* pcm, uint64_t sample_frames, uint32_t format, uint32_t channels,
+                         uint32_t channel, const mgx_outputs* o) {
+  if (!p || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL plan or outputs");
+  const uint32_t bps = pcm_bytes(format);
+  if (!bps) return fail(MGX_E_INVALID_ARGUMENT, "unknown PCM format %u", format);
+  if (channels == 0 || channel >= channels) return fail(MGX_E_INVALID_ARGUMENT, "channel %u of %u", channel, channels);
+  if ((o->complex_real == nullptr) != (o->complex_imag == nullptr))
+    return fail(MGX_E_INVALID_ARGUMENT, "complex_real and complex_imag must be given together");
+  const int n = p->n;
+  const uint64_t nframes = sample_frames / (uint64_t)n;
+  if (nframes == 0) return MGX_OK;
+  if (!pcm) return fail(MGX_E_INVALID_ARGUMENT, "pcm is NULL");
+  const uint64_t align = (uint64_t)bps * channels;
+  const uint64_t chunk_bytes = std::min<uint64_t>(nframes, kHostChunk) * n * align;
+  if (p->s_pcm_bytes < chunk_bytes) {
+    if (p->s_pcm) (void)hipFree(p->s_pcm);
+    p->s_pcm = nullptr;
+    p->s_pcm_bytes = 0;
+    hipError_t e = hipSetDevice(p->d.device);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p->s_pcm), chunk_bytes);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging PCM)");
+    p->s_pcm_bytes = chunk_bytes;
+  }
+  const unsigned char* src = static_cast<const unsigned char*>(pcm);
+  return extract_host_chunked(p, nframes, o, [&](uint64_t f0, uint64_t cnt) {
+    const uint64_t bytes = cnt * n * align;
+    hipError_t e = hipMemcpy(p->s_pcm, src + f0 * n * align, bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(pcm)");
+    e = mgx::launch_pcm_decode(p->s_pcm, cnt * n, format, channels, channel, p->s_frames, nullptr);
+    return e == hipSuccess ? MGX_OK : hip_fail(e, "PCM decode launch");
+  });
 }
 
 int mgx_synth_frames_device(float* frames, uint64_t nframes, uint32_t n, uint64_t seed, uint64_t first_frame, void* stream) {

@@ -11,6 +11,16 @@
 //   process(signal)                 push one buffer (what onaudioprocess does, :69-91)
 //   getBatch(features, frames)      frames: Float32Array(F * bufferSize) -> SoA typed arrays
 //   getBatchAsync(features, frames) same, off the JS thread (napi_async_work)
+//   getBatchWav(features, wavBytes[, channel]) / getBatchWavAsync(...)
+//                                   every full buffer of a .wav file (RIFF walk in C, raw PCM
+//                                   decoded on the device: decodeAudioData's scaling)
+//   Meyda.readWav(wavBytes)         the header: {pcmFormat, channels, sampleRate, sampleFrames, ...}
+//   flush()                         deliver buffered callbacks now (options.batchFrames > 1)
+//
+// Streaming (start/stop, src/meyda.js:69-91,233-241): with options.batchFrames = K > 1
+// the buffers pushed by process() are queued and extracted K at a time in one launch;
+// the callback still runs once per buffer, in order, with that buffer's features
+// (latency of up to K buffers for K-fold fewer launches). stop() flushes the queue.
 //
 // Every built-in feature is computed by libmeyda_gpu.so through the N-API addon.
 // Differences from the snapshot (documented in INTEGRATION.md): the FFT runs per
@@ -50,7 +60,10 @@ class Meyda {
     this.sampleRate = audioContext.sampleRate;
     this.options = Object.assign({
       precision: 'faithful', mode: 'per_buffer_fft', numMelBands: 26, numMfccCoeffs: 13, device: 0,
+      batchFrames: 1,
     }, options || {});
+    this._ring = null;        // queued buffers (batchFrames > 1)
+    this._ringCount = 0;
     this.featureExtractors = {}; // user plugins: fn(bufferSize, m) or {process(signal)}
     this.EXTRACTION_STARTED = false;
     this._featuresToExtract = null;
@@ -104,9 +117,41 @@ class Meyda {
     }
     this.signal = signal;
     this._frame = null;
-    if (typeof this._callback === 'function' && this.EXTRACTION_STARTED) {
+    if (typeof this._callback !== 'function' || !this.EXTRACTION_STARTED) return;
+    const K = this.options.batchFrames | 0;
+    if (K <= 1) {
       this._callback(this.get(this._featuresToExtract));
+      return;
     }
+    if (!this._ring) this._ring = new Float32Array(K * this.bufferSize);
+    this._ring.set(signal, this._ringCount * this.bufferSize);
+    if (++this._ringCount === K) this.flush();
+  }
+
+  // Extract every queued buffer in one launch and run the callback for each, in order.
+  flush() {
+    const count = this._ringCount;
+    if (!count) return;
+    this._ringCount = 0;
+    const list = this._featuresToExtract;
+    const names = typeof list === 'string' ? [list] : Array.prototype.slice.call(list || []);
+    const plugins = names.some((n) => this.featureExtractors[n]);
+    const gpu = names.filter((n) => GPU_FEATURES.has(n) && !this.featureExtractors[n]);
+    if (plugins) gpu.push('amplitudeSpectrum', 'complexSpectrum', 'loudness');
+    const N = this.bufferSize;
+    const frames = this._ring.slice(0, count * N);
+    const r = gpu.length ? addon.extract(this._plan(), frames, gpu) : {};
+    const keep = this.signal;
+    for (let i = 0; i < count; i++) {
+      const sig = frames.subarray(i * N, (i + 1) * N);
+      this.signal = sig;
+      this._frame = {};
+      for (const n of new Set(gpu)) this._frame[n] = frameValue(n, r, i, N, this.options.numMfccCoeffs);
+      const out = typeof list === 'string' ? this._value(list) : this.get(names);
+      this._callback(out);
+    }
+    this.signal = keep;
+    this._frame = null;
   }
 
   setSource(_src) {
@@ -119,6 +164,7 @@ class Meyda {
   }
 
   stop() {
+    if (this._ringCount) this.flush();  // queued buffers are still delivered
     this._featuresToExtract = null;
     this.EXTRACTION_STARTED = false;
   }
@@ -193,6 +239,19 @@ class Meyda {
   getBatchAsync(features, frames) {
     const names = checkBatchNames(features);
     return addon.extractAsync(this._plan(), toF32(frames), names);
+  }
+
+  // Every full buffer of a .wav file (Buffer / Uint8Array / ArrayBuffer), channel `channel`.
+  getBatchWav(features, wavBytes, channel) {
+    return addon.extractWav(this._plan(), wavBytes, checkBatchNames(features), channel | 0);
+  }
+
+  getBatchWavAsync(features, wavBytes, channel) {
+    return addon.extractWavAsync(this._plan(), wavBytes, checkBatchNames(features), channel | 0);
+  }
+
+  static readWav(wavBytes) {
+    return addon.wavParse(wavBytes);
   }
 
   // Per-frame view of a batch result, in the shapes get() returns.

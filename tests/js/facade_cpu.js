@@ -82,4 +82,16 @@ check('no CPU fallback', () => {
   assert.strictEqual(logged, 2);
 });
 
+check('readWav (RIFF walk in the library, no device)', () => {
+  const { wavS16 } = require('./wav');
+  const codes = new Int16Array(2 * 3000).map((_, i) => (i * 37) % 2000 - 1000);
+  const info = Meyda.readWav(wavS16(codes, 2, 22050));
+  assert.strictEqual(info.pcmFormat, 's16');
+  assert.strictEqual(info.channels, 2);
+  assert.strictEqual(info.sampleRate, 22050);
+  assert.strictEqual(info.sampleFrames, 3000);
+  assert.strictEqual(info.dataOffset, 12 + 8 + 16 + 8 + 4 + 8);
+  assert.throws(() => Meyda.readWav(Buffer.from('not a wav file at all')), /RIFF/);
+});
+
 console.log('facade_cpu: ' + n + ' checks passed');

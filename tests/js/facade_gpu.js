@@ -99,6 +99,50 @@ check('start()/stop() streaming callback', () => {
   m.dispose();
 });
 
+check('batched streaming (batchFrames = 4): callbacks per buffer, in order, equal to get()', () => {
+  const seen = [];
+  const m = new Meyda(ctx, null, 512, (feat) => seen.push(feat), { batchFrames: 4 });
+  const list = ['rms', 'zcr', 'spectralCentroid', 'mfcc', 'loudness'];
+  m.start(list);
+  for (let i = 0; i < 10; i++) m.process(frameOf(g, i));
+  assert.strictEqual(seen.length, 8);           // two full batches delivered
+  m.stop();                                     // the last 2 queued buffers are flushed
+  assert.strictEqual(seen.length, 10);
+  const ref = new Meyda(ctx, null, 512);
+  for (let i = 0; i < 10; i++) {
+    ref.process(frameOf(g, i));
+    const r = ref.get(list);
+    for (const k of ['rms', 'zcr', 'spectralCentroid']) assert.strictEqual(seen[i][k], r[k], k + ' frame ' + i);
+    assert.deepStrictEqual(Array.from(seen[i].mfcc), Array.from(r.mfcc));
+    assert.strictEqual(seen[i].loudness.total, r.loudness.total);
+  }
+  m.dispose();
+  ref.dispose();
+});
+
+check('getBatchWav: .wav bytes -> device decode -> features', () => {
+  const { wavS16 } = require('./wav');
+  const idx = [];
+  g.labels.forEach((l, i) => { if (l.startsWith('sound1')) idx.push(i); });
+  const codes = new Int16Array(idx.length * 512 * 2);   // stereo: channel 1 holds the audio
+  idx.forEach((fi, j) => {
+    const x = frameOf(g, fi);
+    for (let t = 0; t < 512; t++) codes[2 * (j * 512 + t) + 1] = Math.round(x[t] * 32768);
+  });
+  const m = new Meyda(ctx, null, 512);
+  const r = m.getBatchWav(['rms', 'zcr', 'mfcc'], wavS16(codes, 2, 44100), 1);
+  assert.strictEqual(r.rms.length, idx.length);
+  idx.forEach((fi, j) => {
+    close(r.rms[j], g.scalars[fi * S + 0], 1e-5, 0, 'wav rms');
+    assert.strictEqual(r.zcr[j], g.scalars[fi * S + 2]);
+    vecClose(r.mfcc.subarray(j * 13, j * 13 + 13), g.mfcc.subarray(fi * 13, fi * 13 + 13), 'wav mfcc');
+  });
+  return m.getBatchWavAsync(['rms'], wavS16(codes, 2, 44100), 1).then((a) => {
+    assert.deepStrictEqual(Array.from(a.rms), Array.from(r.rms));
+    m.dispose();
+  });
+});
+
 check('windowingFunction = hamming', () => {
   const m = new Meyda(ctx, null, 512);
   m.windowingFunction = 'hamming';

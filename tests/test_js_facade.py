@@ -22,10 +22,10 @@ def run_node(script):
 
 def test_facade_host_side():
     out = run_node("facade_cpu.js")
-    assert "facade_cpu: 6 checks passed" in out
+    assert "facade_cpu: 7 checks passed" in out
 
 
 @pytest.mark.gpu
 def test_facade_on_gpu():
     out = run_node("facade_gpu.js")
-    assert "facade_gpu: 6 checks passed" in out
+    assert "facade_gpu: 8 checks passed" in out
