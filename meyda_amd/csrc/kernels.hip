@@ -72,12 +72,12 @@ struct Geo {
   static constexpr int RB = ilog2c(R);      // register bits
   static constexpr int NPASS = (SB + RB - 1) / RB;
   static constexpr int CH = N / 64;         // 64-sample input chunks per frame
-#ifndef MGX_FB
-  static constexpr int FB = 16;             // frames per workgroup batch (phase 2 works on a batch)
+#ifndef MGX_FPW
+  static constexpr int FPW = 4;             // frames per wave batch (phase 2 works on a wave batch)
 #else
-  static constexpr int FB = MGX_FB;
+  static constexpr int FPW = MGX_FPW;
 #endif
-  static constexpr int FPW = FB / 4;        // frames per wave per batch
+  static constexpr int FB = 4 * FPW;        // frames per workgroup iteration
   // Register budget (VGPRs + AGPRs): 4 waves/SIMD (<= 128) up to N = 1024, where LDS
   // allows 4 workgroups per CU; 2 waves (<= 256) at N = 2048. Without the bound the
   // allocator drifts past the threshold (129 VGPRs, or 251 + 32 AGPRs) and occupancy halves.
@@ -435,12 +435,15 @@ template <int N>
 struct Lds {
   using G = Geo<N>;
   // One slot buffer per wave: FFT exchanges, then the frame's amplitude row, its prefix
-  // sums and the mel segment sums (mel_energies) in turn; phase 2 stages the DCT table there.
+  // sums and the mel segment sums (mel_energies) in turn.
   static constexpr size_t slot_off = 0;
   static constexpr size_t slot_bytes = (size_t)4 * G::SLOT_PHYS * 8;
   static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2 + 64) * 4, "mel scratch must fit");
+  // Frame records: FPW per wave.
   static constexpr size_t rec_off = slot_off + slot_bytes;
-  static constexpr size_t bytes = rec_off + (size_t)G::FB * sizeof(FrameRec);
+  // The DCT table (mfcc.js:67-83), staged once per workgroup.
+  static constexpr size_t dct_off = rec_off + (size_t)G::FB * sizeof(FrameRec);
+  static constexpr size_t bytes = dct_off + (size_t)kMaxCoeffs * kMaxMel * 4;
 };
 
 // DPP move of one dword (bound_ctrl: lanes without a source read 0).
@@ -794,15 +797,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   using G = Geo<N>;
   using PG = PassGeo<N>;
   using LY = Lds<N>;
-  constexpr int R = G::R, CH = G::CH, FB = G::FB, FPW = G::FPW;
+  constexpr int R = G::R, CH = G::CH, FPW = G::FPW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
-  FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off);
+  float* dct_lds = reinterpret_cast<float*>(smem + LY::dct_off);
 
-  const int lane = threadIdx.x & 63, tid = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float2* buf = slot_all + wave * G::SLOT_PHYS;
+  FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off) + wave * FPW;  // this wave's records
   KArgs* ap = args_ptr();
+
+  // The DCT table, once per workgroup (the only workgroup barrier of the kernel).
+  if (ap->need_spectrum && ap->need_mfcc) {
+    const int nt = ap->ncoef * ap->nfilt;
+    const auto dct = gbl(ap->t.dct);
+    for (int i = threadIdx.x; i < nt; i += kThreads) dct_lds[i] = dct[i];
+  }
+  lds_barrier();
 
   int lp[G::NPASS];
 #pragma unroll
@@ -815,48 +827,53 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   }
   const bool dc_lane = lp[G::NPASS - 1] == 0;
 
+  // Every wave works through its own batches of FPW consecutive frames: phase 1 per
+  // frame, then phase 2 over the batch, with wave-level synchronisation only.
   const uint64_t nf = ap->num_frames;
-  const uint64_t nb = (nf + FB - 1) / FB;
+  const uint64_t nb = (nf + FPW - 1) / FPW;
+  const uint64_t wstride = (uint64_t)gridDim.x * 4;
   // Register prefetch: the next frame of this wave is loaded while this one is processed.
   // Loads are unconditional (the frame index is clamped; results of frames past the end
   // are never stored), so they issue back to back with no branches or waits between them.
   auto load = [&](float (&xv)[CH], uint64_t b, int j) {
-    uint64_t f = b * FB + j * 4 + wave;
+    uint64_t f = b * FPW + j;
     f = f < nf ? f : nf - 1;
     const auto xin = gbl(args_ptr()->frames) + f * (uint64_t)N;
 #pragma unroll
     for (int c = 0; c < CH; ++c) xv[c] = xin[c * 64 + lane];
   };
   float xn[CH];
-  load(xn, blockIdx.x, 0);
+  const uint64_t b0 = (uint64_t)blockIdx.x * 4 + wave;
+  load(xn, b0, 0);
 
-  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
-    const uint64_t f0 = b * FB;
+  for (uint64_t b = b0; b < nb; b += wstride) {
+    const uint64_t f0 = b * FPW;
     // ------------------------------------------------------------- phase 1
     for (int j = 0; j < FPW; ++j) {
-      const int fb = j * 4 + wave;
-      const uint64_t f = f0 + fb;
+      const uint64_t f = f0 + j;
       float x[CH];
 #pragma unroll
       for (int c = 0; c < CH; ++c) x[c] = xn[c];
       if (j + 1 < FPW) load(xn, b, j + 1);
-      else load(xn, b + gridDim.x, 0);
-      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, fb, f, f < nf, lane, lp, kl, dc_lane, buf, recs);
+      else load(xn, b + wstride, 0);
+      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, recs);
     }
-    lds_barrier();
+    wave_sync();
 
 #ifdef MGX_ABL_NO_PHASE2
     if (opaque(0)) {
 #endif
     // ------------------------------------------------------------- phase 2
-    // Thread ids and the argument pointer are re-derived so that nothing phase 2
-    // needs is hoisted out of the batch loop (it would stay live across the FFT).
+    // Lane ids and the argument pointer are re-derived so that nothing phase 2 needs is
+    // hoisted out of the batch loop (it would stay live across the FFT).
     {
       KArgs* q = args_ptr();
-      const int t2 = opaque(tid);
+      const int l2 = opaque(lane);
       if (ABL_ON(LOUD2) && q->need_spectrum && q->need_loudness) {
         // 32 lanes per frame (24 bands + 8 idle), so a frame's reductions stay in two DPP rows.
-        for (int i = t2; i < FB * 32; i += kThreads) {
+#pragma unroll
+        for (int i0 = 0; i0 < FPW * 32; i0 += 64) {
+          const int i = i0 + l2;
           const int fb = i >> 5, bnd = i & 31;
           const uint64_t f = f0 + fb;
           const bool live = bnd < kBark;
@@ -889,39 +906,30 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         }
       }
       if (ABL_ON(COMB) && q->need_spectrum && q->need_mfcc) {
-        // stage the DCT table in the (now idle) slot buffers for the next step
-        const int nt = q->ncoef * q->nfilt;
-        if (nt <= (int)(LY::slot_bytes / 4)) {
-          const auto dct = gbl(q->t.dct);
-          float* dl = reinterpret_cast<float*>(slot_all);
-          for (int i = t2; i < nt; i += kThreads) dl[i] = dct[i];
-        }
         // mfcc.js:64 Math.log of the band energies, stored to Float32Array
         const int nfilt = q->nfilt;
-        for (int i = t2; i < FB * nfilt; i += kThreads) {
-          const int band = i / FB, fb = i % FB;
+        for (int i = l2; i < FPW * nfilt; i += 64) {
+          const int band = i / FPW, fb = i % FPW;
           recs[fb].lm[band] = ln_f32(recs[fb].lm[band]);
         }
       }
     }
-    lds_barrier();
+    wave_sync();
     {
       KArgs* q = args_ptr();
-      const int t2 = opaque(tid);
+      const int l2 = opaque(lane);
       if (ABL_ON(DCT) && q->need_spectrum && q->need_mfcc) {
         const int nc = q->ncoef, nfilt = q->nfilt;
-        const bool staged = nc * nfilt <= (int)(LY::slot_bytes / 4);
-        for (int i = t2; i < FB * nc; i += kThreads) {
-          const int c = i / FB, fb = i % FB;
+        for (int i = l2; i < FPW * nc; i += 64) {
+          const int c = i / FPW, fb = i % FPW;
           const uint64_t f = f0 + fb;
-          const double v = staged ? dct_sum(reinterpret_cast<const float*>(slot_all), recs[fb].lm, c, nc, nfilt)
-                                  : dct_sum(gbl(q->t.dct), recs[fb].lm, c, nc, nfilt);
+          const double v = dct_sum(dct_lds, recs[fb].lm, c, nc, nfilt);
           if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(v / nc);
         }
       }
-      // the other scalar features: one thread per (feature, frame)
-      for (int i = t2; ABL_ON(FIN) && i < MGX_LOUDNESS_TOTAL * FB; i += kThreads) {
-        const int sc = i / FB, fb = i % FB;
+      // the other scalar features: one lane per (feature, frame)
+      for (int i = l2; ABL_ON(FIN) && i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {
+        const int sc = i / FPW, fb = i % FPW;
         const uint64_t f = f0 + fb;
         void* dst = q->out.scalars[sc];
         if (f >= q->num_frames || dst == nullptr) continue;
@@ -933,7 +941,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
 #ifdef MGX_ABL_NO_PHASE2
     }
 #endif
-    lds_barrier();
+    wave_sync();  // records and slot buffer are reused by the next batch
   }
 }
 
