@@ -329,7 +329,9 @@ __device__ __forceinline__ double wave_sum(double v) {
   v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
   v += dpp_d<0x141>(v);  // row_half_mirror
   v += dpp_d<0x140>(v);  // row_mirror: every lane holds its row's sum
-  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+  v += dpp_d<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3 hold rows 0+1, 2+3
+  v += dpp_d<0x143, 0xC>(v);  // row_bcast:31 -> row 3 holds the total
+  return readlane_d(v, 63);
 }
 
 // Inclusive prefix sum over the lanes.
@@ -372,7 +374,7 @@ struct FrameRec {
   double ln2sum;    // sum_k log2 a_k
   double energy;    // sum x^2
   double band[kBark];
-  float lm[kMaxMel];  // mel band energies, then their logs
+  float lm[kMaxMel];  // mel band energies, then their logs (zero-padded to a multiple of 8)
   int zcr;
   int roll_m;
   double pad;       // 520 bytes: phase 2 reads across frames hit distinct LDS banks (512 would not)
@@ -736,60 +738,63 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
 }
 
-// mfcc.js:85-93: coefficient c of one frame, sum_n dct[c][n] * lm[n] in double (the order
-// is sequential as written; loads are clamped and unconditional so each group of 8 issues together).
-template <typename P>
-__device__ __forceinline__ double dct_sum(P dct, const float* lm, int c, int nc, int nfilt) {
+// mfcc.js:85-93: coefficient c of one frame, sum_n dct[c][n] * lm[n] in double, in the
+// reference's sequential order. The product of two floats is exact in double, so an FMA
+// equals the reference's multiply-then-add. lm and the LDS table are zero-padded to a
+// multiple of 8 bands (0 * 0 adds nothing), so groups of 8 loads issue together.
+__device__ __forceinline__ double dct_sum(const float* dct, const float* lm, int c, int nc, int nfilt) {
   double v = 0.0;
   for (int n0 = 0; n0 < nfilt; n0 += 8) {
     float dv[8], lv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int nn = n0 + u < nfilt ? n0 + u : nfilt - 1;
-      dv[u] = dct[c + nn * nc];
-      lv[u] = lm[nn];
+      dv[u] = dct[c + (n0 + u) * nc];
+      lv[u] = lm[n0 + u];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const double t = v + (double)dv[u] * (double)lv[u];
-      v = n0 + u < nfilt ? t : v;
-    }
+    for (int u = 0; u < 8; ++u) v = __builtin_fma((double)dv[u], (double)lv[u], v);
   }
   return v;
 }
 
-// One scalar feature of a frame from its phase-1 record. Formulas as written in the
-// reference extractors; scalars not requested never reach here.
+// One of the ten spectral/time scalars of a frame from its phase-1 record, formulas as
+// written in the reference extractors. Branch-free: every lane evaluates the shared terms
+// (moments, spread) and selects its feature's numerator and denominator, so a wave
+// holding ten different features runs one instruction stream.
 template <int N>
-__device__ __attribute__((noinline)) double scalar_value(KArgs* q, const FrameRec& rc, int sc) {
+__device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int sc) {
   constexpr int L = N / 2;
   const double S0 = rc.S[0];
-  switch (sc) {
-    case MGX_ENERGY: return rc.energy;                       // energy.js
-    case MGX_RMS: return sqrt(rc.energy / N);                // rms.js
-    case MGX_ZCR: return (double)rc.zcr;                     // zcr.js
-    case MGX_SPECTRAL_CENTROID: return rc.S[1] / S0;         // spectralCentroid.js -> utils.js:1-11 mu(1)
-    case MGX_SPECTRAL_FLATNESS:                              // spectralFlatness.js: geometric / arithmetic mean
-      return exp(rc.ln2sum * kLn2 / L) * L / S0;
-    case MGX_SPECTRAL_SLOPE: {                               // spectralSlope.js:9-21
-      const double afs = (q->sample_rate / N) * rc.S[1];
-      return (L * afs - q->freq_sum * S0) / (S0 * (q->pow_freq_sum - q->freq_sum * q->freq_sum));
-    }
-    case MGX_SPECTRAL_ROLLOFF: return (double)rc.roll_m * q->nyq_bin;  // spectralRolloff.js:6-15
-    case MGX_SPECTRAL_SPREAD:                                // spectralSpread.js
-    case MGX_SPECTRAL_SKEWNESS:                              // spectralSkewness.js
-    case MGX_SPECTRAL_KURTOSIS: {                            // spectralKurtosis.js (6 mu1 mu2 as written)
-      const double m1 = rc.S[1] / S0, m2 = rc.S[2] / S0;
-      const double var = m2 - m1 * m1, sd = sqrt(var);
-      if (sc == MGX_SPECTRAL_SPREAD) return sd;
-      const double m3 = rc.S[3] / S0;
-      if (sc == MGX_SPECTRAL_SKEWNESS) return (2.0 * m1 * m1 * m1 - 3.0 * m1 * m2 + m3) / (sd * sd * sd);
-      const double m4 = rc.S[4] / S0;
-      return (-3.0 * m1 * m1 * m1 * m1 + 6.0 * m1 * m2 - 4.0 * m1 * m3 + m4) / (sd * sd * sd * sd);
-    }
-    default:
-      return 0.0;  // loudness scalars are written in phase 2's loudness step
+  // utils.js:1-11 mu(p) = sum k^p a_k / sum a_k
+  const double m1 = rc.S[1] / S0, m2 = rc.S[2] / S0, m3 = rc.S[3] / S0, m4 = rc.S[4] / S0;
+  const double sd = sqrt(m2 - m1 * m1);  // spectralSpread.js
+  double num, den = 1.0;
+  switch (sc) {  // selects only (no divergent code: every case is a few operands)
+    case MGX_RMS: num = rc.energy * (1.0 / N); break;  // rms.js: sqrt(sum / N), N a power of 2
+    case MGX_ENERGY: num = rc.energy; break;           // energy.js
+    case MGX_ZCR: num = (double)rc.zcr; break;         // zcr.js
+    case MGX_SPECTRAL_CENTROID: num = m1; break;       // spectralCentroid.js
+    case MGX_SPECTRAL_FLATNESS:                        // spectralFlatness.js: geometric / arithmetic mean
+      num = exp(rc.ln2sum * kLn2 / L) * L;
+      den = S0;
+      break;
+    case MGX_SPECTRAL_SLOPE:                           // spectralSlope.js:9-21
+      num = L * ((q->sample_rate / N) * rc.S[1]) - q->freq_sum * S0;
+      den = S0 * (q->pow_freq_sum - q->freq_sum * q->freq_sum);
+      break;
+    case MGX_SPECTRAL_ROLLOFF: num = (double)rc.roll_m * q->nyq_bin; break;  // spectralRolloff.js:6-15
+    case MGX_SPECTRAL_SPREAD: num = sd; break;
+    case MGX_SPECTRAL_SKEWNESS:                        // spectralSkewness.js
+      num = 2.0 * m1 * m1 * m1 - 3.0 * m1 * m2 + m3;
+      den = sd * sd * sd;
+      break;
+    default:                                           // spectralKurtosis.js (6 mu1 mu2 as written)
+      num = -3.0 * m1 * m1 * m1 * m1 + 6.0 * m1 * m2 - 4.0 * m1 * m3 + m4;
+      den = sd * sd * sd * sd;
+      break;
   }
+  const double v = num / den;
+  return sc == MGX_RMS ? sqrt(v) : v;
 }
 
 template <int N, bool FAITH, bool LITERAL>
@@ -810,9 +815,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
 
   // The DCT table, once per workgroup (the only workgroup barrier of the kernel).
   if (ap->need_spectrum && ap->need_mfcc) {
-    const int nt = ap->ncoef * ap->nfilt;
+    const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
     const auto dct = gbl(ap->t.dct);
-    for (int i = threadIdx.x; i < nt; i += kThreads) dct_lds[i] = dct[i];
+    for (int i = threadIdx.x; i < ntp; i += kThreads) dct_lds[i] = i < nt ? dct[i] : 0.0f;
   }
   lds_barrier();
 
@@ -884,17 +889,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
           if (live && f < q->num_frames && q->out.loudness_specific) gbl(q->out.loudness_specific)[f * kBark + bnd] = sp;
           // loudness.js:67-69 total; perceptualSpread.js:7-12 max; perceptualSharpness.js:7-14
           // (off-by-one spec[i+1] for i < 15, then the constant 0.066 e^{0.171 (i+1)} tail).
-          double tot = sp, mx = sp, sh = (bnd >= 1 && bnd <= 15) ? (double)bnd * sp : 0.0;
-          tot += dpp_d<0xB1>(tot); mx = fmax(mx, dpp_d<0xB1>(mx)); sh += dpp_d<0xB1>(sh);
-          tot += dpp_d<0x4E>(tot); mx = fmax(mx, dpp_d<0x4E>(mx)); sh += dpp_d<0x4E>(sh);
-          tot += dpp_d<0x141>(tot); mx = fmax(mx, dpp_d<0x141>(mx)); sh += dpp_d<0x141>(sh);
-          tot += dpp_d<0x140>(tot); mx = fmax(mx, dpp_d<0x140>(mx)); sh += dpp_d<0x140>(sh);
+          // total in double (perceptualSpread's (total - max) cancels); max exact in float32;
+          // the sharpness weighted sum in float32 (a plain sum of positive terms).
+          double tot = sp;
+          float mx = sp, sh = (bnd >= 1 && bnd <= 15) ? (float)bnd * sp : 0.0f;
+          tot += dpp_d<0xB1>(tot); mx = fmaxf(mx, dpp_f<0xB1>(mx)); sh += dpp_f<0xB1>(sh);
+          tot += dpp_d<0x4E>(tot); mx = fmaxf(mx, dpp_f<0x4E>(mx)); sh += dpp_f<0x4E>(sh);
+          tot += dpp_d<0x141>(tot); mx = fmaxf(mx, dpp_f<0x141>(mx)); sh += dpp_f<0x141>(sh);
+          tot += dpp_d<0x140>(tot); mx = fmaxf(mx, dpp_f<0x140>(mx)); sh += dpp_f<0x140>(sh);
           // rows 2r and 2r+1 hold one frame: row_bcast:15 adds row 2r's total into row 2r+1
-          tot += dpp_d<0x142, 0xA>(tot); mx = fmax(mx, dpp_d<0x142, 0xA>(mx)); sh += dpp_d<0x142, 0xA>(sh);
+          tot += dpp_d<0x142, 0xA>(tot); mx = fmaxf(mx, dpp_f<0x142, 0xA>(mx)); sh += dpp_f<0x142, 0xA>(sh);
           if (bnd == 31 && f < q->num_frames) {
-            sh += q->sharp_tail_sum;
-            const double ps = (tot - mx) / tot;
-            const double sv[3] = {tot, ps * ps, sh * (0.11 / tot)};
+            const double ps = (tot - (double)mx) / tot;
+            const double sv[3] = {tot, ps * ps, ((double)sh + q->sharp_tail_sum) * (0.11 / tot)};
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
               void* dst = q->out.scalars[MGX_LOUDNESS_TOTAL + k];
@@ -907,10 +914,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       }
       if (ABL_ON(COMB) && q->need_spectrum && q->need_mfcc) {
         // mfcc.js:64 Math.log of the band energies, stored to Float32Array
-        const int nfilt = q->nfilt;
-        for (int i = l2; i < FPW * nfilt; i += 64) {
+        const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
+        for (int i = l2; i < FPW * nfp; i += 64) {
           const int band = i / FPW, fb = i % FPW;
-          recs[fb].lm[band] = ln_f32(recs[fb].lm[band]);
+          recs[fb].lm[band] = band < nfilt ? ln_f32(recs[fb].lm[band]) : 0.0f;  // padding for dct_sum
         }
       }
     }
