@@ -82,7 +82,8 @@ struct Geo {
   // allows 4 workgroups per CU; 2 waves (<= 256) at N = 2048. Without the bound the
   // allocator drifts past the threshold (129 VGPRs, or 251 + 32 AGPRs) and occupancy halves.
   static constexpr int WPE = N <= 1024 ? 4 : 2;
-  static constexpr int SLOT_PHYS = L + (L >> 4) + 2;  // exchange layout (phys); also >= L doubles
+  // exchange layout (phys) needs L + L/16 + 2 slots (also >= the L-double prefix row)
+  static constexpr int SLOT_PHYS = L + (L >> 4) + 2;
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
 
@@ -371,7 +372,7 @@ __device__ __forceinline__ float slot_amp(float re, float im) {
 
 struct FrameRec {
   double S[5];      // sum_k k^p a_k, p = 0..4 (S[0] = sum a_k)
-  double ln2sum;    // sum_k log2 a_k
+  double ln2sum;    // sum_k log2 a_k (must follow S[4]: written as (&S[1])[4])
   double energy;    // sum x^2
   double band[kBark];
   float lm[kMaxMel];  // mel band energies, then their logs (zero-padded to a multiple of 8)
@@ -441,11 +442,14 @@ struct Lds {
   static constexpr size_t slot_off = 0;
   static constexpr size_t slot_bytes = (size_t)4 * G::SLOT_PHYS * 8;
   static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2 + 64) * 4, "mel scratch must fit");
+  // Per wave, the 5 x 64 table of moment partials (transposed reduction, N <= 512).
+  static constexpr size_t mom_off = slot_off + slot_bytes;
+  static constexpr size_t mom_bytes = N <= 512 ? (size_t)4 * 5 * 64 * 8 : 0;
   // Frame records: FPW per wave.
-  static constexpr size_t rec_off = slot_off + slot_bytes;
-  // The DCT table (mfcc.js:67-83), staged once per workgroup.
+  static constexpr size_t rec_off = mom_off + mom_bytes;
+  // The DCT table (mfcc.js:67-83), staged once per workgroup, sized per plan.
   static constexpr size_t dct_off = rec_off + (size_t)G::FB * sizeof(FrameRec);
-  static constexpr size_t bytes = dct_off + (size_t)kMaxCoeffs * kMaxMel * 4;
+  static size_t bytes(int ncoef, int nfilt) { return dct_off + (size_t)ncoef * ((nfilt + 7) & ~7) * 4; }
 };
 
 // DPP move of one dword (bound_ctrl: lanes without a source read 0).
@@ -558,7 +562,7 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
 template <int N, bool FAITH, bool LITERAL>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
                                              int lane, const int (&lp)[Geo<N>::NPASS], const int (&kl)[Geo<N>::R],
-                                             bool dc_lane, float2* buf, FrameRec* recs) {
+                                             bool dc_lane, float2* buf, double* mom, FrameRec* recs) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
@@ -701,6 +705,26 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     l2f += log2f(av[jj]);
   }
   wave_sync();  // every lane has read the amplitude row: the buffer takes the prefix sums next
+  FrameRec& rec = recs[fb];
+  // Moments S1..S4 (bin-offset polynomial shift of the local partials) and sum log2 a:
+  // five sums over the lanes. Up to N = 512 (5+ waves per SIMD) they go through one LDS
+  // transpose: lane l writes column l of a 5 x 64 table; after the prefix scan, lanes
+  // 0..39 each add 8 entries (stride 8) of one row and 3 DPP steps finish the row in
+  // 8-lane groups. At N >= 1024 (4 waves per SIMD) the LDS round trip measured slower
+  // than five DPP wave sums, which are used there.
+  constexpr bool kMomLds = N <= 512;
+  const double bb = (double)(R * lane), b2 = bb * bb, b3 = b2 * bb, b4 = b3 * bb;
+  const double P1 = __builtin_fma(bb, T0, T1);
+  const double P2 = T2 + 2.0 * bb * T1 + b2 * T0;
+  const double P3 = T3 + 3.0 * bb * T2 + 3.0 * b2 * T1 + b3 * T0;
+  const double P4 = T4 + 4.0 * bb * T3 + 6.0 * b2 * T2 + 4.0 * b3 * T1 + b4 * T0;
+  if constexpr (kMomLds) {
+    mom[0 * 64 + lane] = P1;
+    mom[1 * 64 + lane] = P2;
+    mom[2 * 64 + lane] = P3;
+    mom[3 * 64 + lane] = P4;
+    mom[4 * 64 + lane] = (double)l2f;
+  }
   // prefix P(k) = sum_{i<k} a_i: lane-exclusive offset + local prefix
   const double incl = wave_inclusive_scan(T0);
   const double excl = dpp_d<0x138>(incl);  // wave_shr:1 (lane 0 reads 0)
@@ -711,26 +735,35 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   double pk = excl;  // P(R lane + jj), accumulated again rather than kept (registers)
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) {
-    pbuf[R * lane + jj] = pk;  // the slot buffer is free again (reads above completed)
+    pbuf[R * lane + jj] = pk;
     cnt += __popcll(__ballot(pk <= thr));
     pk += (double)av[jj];
   }
   const int roll_m = (total > thr) ? cnt - 1 : L;
-  const double bb = (double)(R * lane), b2 = bb * bb, b3 = b2 * bb, b4 = b3 * bb;
-  const double S1 = wave_sum(__builtin_fma(bb, T0, T1));
-  const double S2 = wave_sum(T2 + 2.0 * bb * T1 + b2 * T0);
-  const double S3 = wave_sum(T3 + 3.0 * bb * T2 + 3.0 * b2 * T1 + b3 * T0);
-  const double S4 = wave_sum(T4 + 4.0 * bb * T3 + 6.0 * b2 * T2 + 4.0 * b3 * T1 + b4 * T0);
-  const double l2 = wave_sum((double)l2f);
-  wave_sync();
-  FrameRec& rec = recs[fb];
+  if constexpr (kMomLds) {
+    wave_sync();
+    const int row = lane < 40 ? lane >> 3 : 0;
+    const double* src = mom + row * 64 + (lane & 7);  // entries g, g+8, ..., g+56: conflict-free
+    double t = ((src[0] + src[8]) + (src[16] + src[24])) + ((src[32] + src[40]) + (src[48] + src[56]));
+    t += dpp_d<0xB1>(t);   // quad_perm [1,0,3,2]
+    t += dpp_d<0x4E>(t);   // quad_perm [2,3,0,1]
+    t += dpp_d<0x141>(t);  // row_half_mirror: each 8-lane group holds its row's total
+    if (lane < 40 && (lane & 7) == 0) (&rec.S[1])[row] = t;  // S[1..4], then ln2sum
+  } else {
+    const double S1 = wave_sum(P1), S2 = wave_sum(P2), S3 = wave_sum(P3), S4 = wave_sum(P4);
+    const double l2 = wave_sum((double)l2f);
+    wave_sync();
+    if (lane == 0) {
+      rec.S[1] = S1; rec.S[2] = S2; rec.S[3] = S3; rec.S[4] = S4;
+      rec.ln2sum = l2;
+    }
+  }
   if (lane < kBark) {
     const auto lim = gbl(ap->t.bblim);
     rec.band[lane] = pbuf[lim[lane + 1]] - pbuf[lim[lane]];
   }
   if (lane == 0) {
-    rec.S[0] = total; rec.S[1] = S1; rec.S[2] = S2; rec.S[3] = S3; rec.S[4] = S4;
-    rec.ln2sum = l2;
+    rec.S[0] = total;
     rec.roll_m = roll_m;
   }
   if (ABL_ON(MELSCAN) && ap->need_mfcc) mel_energies<N>(ap, av, lane, buf, rec);
@@ -806,6 +839,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
   float* dct_lds = reinterpret_cast<float*>(smem + LY::dct_off);
+  double* mom = reinterpret_cast<double*>(smem + LY::mom_off) + (threadIdx.x >> 6) * (5 * 64);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -861,7 +895,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       for (int c = 0; c < CH; ++c) x[c] = xn[c];
       if (j + 1 < FPW) load(xn, b, j + 1);
       else load(xn, b + wstride, 0);
-      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, recs);
+      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs);
     }
     wave_sync();
 
@@ -996,25 +1030,26 @@ __global__ void pcm_decode_kernel(const unsigned char* __restrict__ pcm, uint64_
 
 template <int N, bool FAITH, bool LITERAL>
 hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
-  const size_t lds = Lds<N>::bytes;
+  const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
   hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL>), dim3(grid), dim3(kThreads), lds, stream, a);
   return hipGetLastError();
 }
 
 template <int N, bool FAITH, bool LITERAL>
-int occupancy_n() {
+int occupancy_n(size_t lds) {
   int blocks = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL>, kThreads,
-                                                   Lds<N>::bytes) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL>, kThreads, lds) !=
+      hipSuccess)
     return 0;
   return blocks;
 }
 
 template <int N>
-int occupancy_prec(int precision, int mode) {
-  if (mode == MGX_MODE_LITERAL) return occupancy_n<N, true, true>();
-  if (precision == MGX_PRECISION_FAST) return occupancy_n<N, false, false>();
-  return occupancy_n<N, true, false>();
+int occupancy_prec(int precision, int mode, int ncoef, int nfilt) {
+  const size_t lds = Lds<N>::bytes(ncoef, nfilt);
+  if (mode == MGX_MODE_LITERAL) return occupancy_n<N, true, true>(lds);
+  if (precision == MGX_PRECISION_FAST) return occupancy_n<N, false, false>(lds);
+  return occupancy_n<N, true, false>(lds);
 }
 
 template <int N>
@@ -1026,12 +1061,12 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
 
 }  // namespace
 
-size_t extract_lds_bytes(int n) {
+size_t extract_lds_bytes(int n, int ncoef, int nfilt) {
   switch (n) {
-    case 256: return Lds<256>::bytes;
-    case 512: return Lds<512>::bytes;
-    case 1024: return Lds<1024>::bytes;
-    case 2048: return Lds<2048>::bytes;
+    case 256: return Lds<256>::bytes(ncoef, nfilt);
+    case 512: return Lds<512>::bytes(ncoef, nfilt);
+    case 1024: return Lds<1024>::bytes(ncoef, nfilt);
+    case 2048: return Lds<2048>::bytes(ncoef, nfilt);
     default: return 0;
   }
 }
@@ -1046,12 +1081,12 @@ int frames_per_batch(int n) {
   }
 }
 
-int extract_blocks_per_cu(int n, int precision, int mode) {
+int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt) {
   switch (n) {
-    case 256: return occupancy_prec<256>(precision, mode);
-    case 512: return occupancy_prec<512>(precision, mode);
-    case 1024: return occupancy_prec<1024>(precision, mode);
-    case 2048: return occupancy_prec<2048>(precision, mode);
+    case 256: return occupancy_prec<256>(precision, mode, ncoef, nfilt);
+    case 512: return occupancy_prec<512>(precision, mode, ncoef, nfilt);
+    case 1024: return occupancy_prec<1024>(precision, mode, ncoef, nfilt);
+    case 2048: return occupancy_prec<2048>(precision, mode, ncoef, nfilt);
     default: return 0;
   }
 }

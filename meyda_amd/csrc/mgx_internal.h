@@ -48,8 +48,8 @@ hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t firs
                         hipStream_t stream);
 hipError_t launch_pcm_decode(const void* pcm, uint64_t count, uint32_t format, uint32_t channels,
                              uint32_t channel, float* out, hipStream_t stream);
-size_t extract_lds_bytes(int n);
+size_t extract_lds_bytes(int n, int ncoef, int nfilt);
 int frames_per_batch(int n);
-int extract_blocks_per_cu(int n, int precision, int mode);  // resident workgroups per CU
+int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt);  // resident workgroups per CU
 
 }  // namespace mgx

@@ -330,7 +330,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->nyq = d->sample_rate / (2.0 * (L - 1));  // spectralRolloff.js:4
   for (int i = 15; i < mgx::kBark; ++i) p->sharp_tail += 0.066 * exp(0.171 * (i + 1));  // perceptualSharpness.js:10
   // persistent grid: exactly the workgroups that are resident at once
-  p->grid_cap = prop.multiProcessorCount * std::max(1, mgx::extract_blocks_per_cu(n, (int)d->precision, (int)d->mode));
+  p->grid_cap = prop.multiProcessorCount * std::max(1, mgx::extract_blocks_per_cu(n, (int)d->precision, (int)d->mode, (int)d->num_mfcc_coeffs, (int)d->num_mel_bands));
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
