@@ -558,6 +558,41 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
   if (lane + 64 < nf) rec.lm[lane + 64] = mu[lane + 64] + md[lane + 65];
 }
 
+// Bark-band sums and mel energies of a frame with a non-finite amplitude, summed exactly
+// as the reference does (see frame_phase1). The amplitude row is rewritten to the slot buffer.
+template <int N>
+__device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av)[Geo<N>::R], int lane,
+                                                               float2* buf, FrameRec& rec) {
+  constexpr int L = N / 2, R = Geo<N>::R;
+  float* amp = reinterpret_cast<float*>(buf);
+  wave_sync();  // prefix reads (band sums) are done
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) amp[R * lane + jj] = av[jj];
+  wave_sync();
+  if (lane < kBark) {  // loudness.js:47-66: sumArray over [lim_b, lim_{b+1}) in double
+    const auto lim = gbl(ap->t.bblim);
+    double sum = 0.0;
+    for (int k = lim[lane]; k < lim[lane + 1]; ++k) sum += (double)amp[k];
+    rec.band[lane] = sum;
+  }
+  if (ap->need_mfcc) {  // mfcc.js:53-62: every bin, double weight x float power, float32 sum
+    const int nf = ap->nfilt;
+    const auto b = gbl(ap->t.mel_bins);
+    for (int j = lane; j < nf; j += 64) {
+      const int b0 = b[j], b1 = b[j + 1], b2 = b[j + 2];
+      float e = 0.0f;
+      for (int k = 0; k < L; ++k) {
+        double w = 0.0;
+        if (k >= b0 && k < b1) w = (double)(k - b0) / (b1 - b0);
+        if (k >= b1 && k < b2) w = (double)(b2 - k) / (b2 - b1);
+        const float p = amp[k] * amp[k];
+        e = (float)((double)e + w * (double)p);
+      }
+      rec.lm[j] = e;
+    }
+  }
+}
+
 // One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
 template <int N, bool FAITH, bool LITERAL>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
@@ -766,7 +801,17 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     rec.S[0] = total;
     rec.roll_m = roll_m;
   }
-  if (ABL_ON(MELSCAN) && ap->need_mfcc) mel_energies<N>(ap, av, lane, buf, rec);
+  // A non-finite amplitude (Inf/NaN samples, or overflow in the FFT) breaks the prefix
+  // differences (Inf - Inf) and the segment decomposition of the mel sums (the reference's
+  // zero weights turn Inf into NaN in every band). Such frames — wave-uniform, rare — take
+  // the reference's own summation: bark bands bin by bin in double (loudness.js:47-66),
+  // mel bands over all bins in reference order (mfcc.js:53-62).
+  // (total = sum of the amplitudes in double: non-finite iff some amplitude is.)
+  if (!(total < __builtin_huge_val())) {
+    nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
+  } else if (ABL_ON(MELSCAN) && ap->need_mfcc) {
+    mel_energies<N>(ap, av, lane, buf, rec);
+  }
 #endif
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
 }

@@ -20,6 +20,7 @@ struct DevTables {
   const int* bblim;          // 25 bark band limits (loudness.js:24-45)
   const float2* mel_wud;     // N/2: (rising, falling) filter weight of each bin in its segment (mfcc.js:40-51)
   const uint8_t* mel_seg;    // N/2: segment m of each bin (b_m <= k < b_{m+1}); nfilt + 1 = no band
+  const int* mel_bins;       // nfilt + 2 filter edges (mfcc.js:15-38), for the non-finite-frame path
   const float* dct;          // ncoef * nfilt, dct[c + j*ncoef] (mfcc.js:67-83)
 };
 

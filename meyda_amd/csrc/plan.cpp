@@ -336,7 +336,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
                o_twf = carve<float>(off, twf.size()), o_kl = carve<int>(off, L),
                o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<float>(off, mwud.size()),
-               o_seg = carve<uint8_t>(off, mseg.size()), o_dct = carve<float>(off, dct.size());
+               o_seg = carve<uint8_t>(off, mseg.size()), o_dct = carve<float>(off, dct.size()),
+               o_mb = carve<int32_t>(off, bins.size());
   std::vector<unsigned char> host(off, 0);
   auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) memcpy(host.data() + at, src, bytes); };
   put(o_win, d->window == MGX_WINDOW_HAMMING ? ham.data() : han.data(), n * sizeof(float));
@@ -346,6 +347,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   put(o_lim, lim, sizeof lim);
   put(o_mw, mwud.data(), mwud.size() * sizeof(float));
   put(o_seg, mseg.data(), mseg.size());
+  put(o_mb, bins.data(), bins.size() * sizeof(int32_t));
   put(o_dct, dct.data(), dct.size() * sizeof(float));
   e = hipMalloc(reinterpret_cast<void**>(&p->dev), off);
   if (e != hipSuccess) { delete p; return hip_fail(e, "hipMalloc(plan tables)"); }
@@ -359,6 +361,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->t.bblim = reinterpret_cast<const int*>(b + o_lim);
   p->t.mel_wud = reinterpret_cast<const float2*>(b + o_mw);
   p->t.mel_seg = reinterpret_cast<const uint8_t*>(b + o_seg);
+  p->t.mel_bins = reinterpret_cast<const int*>(b + o_mb);
   p->t.dct = reinterpret_cast<const float*>(b + o_dct);
   *out = p;
   return MGX_OK;

@@ -1,0 +1,148 @@
+"""GPU parity beyond the golden fixtures: non-finite and extreme inputs, other sample
+rates, window and mel-band counts, N = 256, and a seeded randomized sweep of plan
+configurations — every case against the CPU oracle (tests/tolerance.py bars; NaN/Inf
+classes must match exactly)."""
+import numpy as np
+import pytest
+
+import tolerance
+
+pytestmark = pytest.mark.gpu
+
+FEATS = ["rms", "energy", "zcr", "spectralCentroid", "spectralFlatness", "spectralSlope",
+         "spectralRolloff", "spectralSpread", "spectralSkewness", "spectralKurtosis", "loudness",
+         "perceptualSpread", "perceptualSharpness", "mfcc", "amplitudeSpectrum"]
+SCALARS = ["rms", "energy", "zcr", "spectralCentroid", "spectralFlatness", "spectralSlope",
+           "spectralRolloff", "spectralSpread", "spectralSkewness", "spectralKurtosis",
+           "loudness.total", "perceptualSpread", "perceptualSharpness"]
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from meyda_amd import capi
+    if capi.device_count() == 0:
+        pytest.fail("no GPU visible to libmeyda_gpu.so")
+    return capi
+
+
+def compare(out, ref, n, sr=44100.0, spectra_exact_min=None):
+    got_s = np.stack([out[k].astype(np.float64) for k in SCALARS], 1)
+    fails = tolerance.check_scalars(got_s, ref["scalars"], ref["amp"], n, sr=sr)
+    assert not fails, fails[:10]
+    a, r = out["amplitudeSpectrum"].astype(np.float64), ref["amp"].astype(np.float64)
+    # Frames where an infinity enters the FFT (an Inf sample, or overflow inside a stage):
+    # the reference's full complex FFT forms 0 * Inf in its j = 0 twiddle product, which
+    # turns the imaginary companion of the real DC / X[N/4] values into NaN; the
+    # half-spectrum network never forms that product, so those two bins can be +-Inf where
+    # the reference has NaN. Every other bin, and every feature (checked
+    # above), matches in class.
+    nonfin = ~np.isfinite(r).all(1)
+    ex = np.zeros(a.shape, bool)
+    ex[:, 0] = nonfin
+    ex[:, a.shape[1] // 2] = nonfin
+    assert np.array_equal(np.isnan(a) & ~ex, np.isnan(r) & ~ex)
+    assert np.array_equal(np.isinf(a) & ~ex, np.isinf(r) & ~ex)
+    assert np.all(~np.isfinite(a[ex]) | ~np.isfinite(r[ex]) | (a[ex] == r[ex]))
+    fin = np.isfinite(r).all(1)
+    bad, exact = tolerance.check_spectra(out["amplitudeSpectrum"][fin], ref["amp"][fin])
+    assert not bad, bad
+    if spectra_exact_min is not None:
+        assert exact >= spectra_exact_min, exact
+    # mfcc and specific loudness: exact policy on finite frames; on non-finite frames every
+    # value the reference leaves finite must match (bands away from bins 0 and N/4), and
+    # every NaN of the reference must be non-finite here.
+    for key, rkey in (("mfcc", "mfcc"), ("loudness.specific", "loudness_specific")):
+        g, rr = out[key], ref[rkey]
+        assert not tolerance.check_vectors(g[~nonfin], rr[~nonfin]), key
+        if nonfin.any():
+            gn, rn = g[nonfin].astype(np.float64), rr[nonfin].astype(np.float64)
+            fin = np.isfinite(rn)
+            assert np.all(np.isfinite(gn[fin])), key
+            with np.errstate(invalid="ignore"):
+                assert np.all(np.abs(gn[fin] - rn[fin]) <= 1e-5 * np.abs(rn[fin]) + 1e-30), key
+            assert np.all(~np.isfinite(gn[~fin])), key
+
+
+def edge_frames(n):
+    rng = np.random.default_rng(5)
+    fr = []
+    x = rng.uniform(-1, 1, n).astype(np.float32)
+    y = x.copy(); y[n // 3] = np.nan; fr.append(y)                    # one NaN sample
+    y = x.copy(); y[7] = np.inf; fr.append(y)                         # one +Inf sample
+    y = x.copy(); y[n - 1] = -np.inf; fr.append(y)                    # -Inf at the end
+    fr.append(np.full(n, np.nan, np.float32))                         # all NaN
+    fr.append(np.full(n, 3.0e38, np.float32))                         # energy overflows
+    fr.append((x * 1e-39).astype(np.float32))                         # denormal samples
+    fr.append(np.where(np.arange(n) % 2 == 0, 1.0, -1.0).astype(np.float32))  # Nyquist
+    y = np.zeros(n, np.float32); y[0] = -0.0; y[1] = 0.0; fr.append(y)          # signed zeros
+    fr.append(np.full(n, 1e-45, np.float32))                          # smallest denormal, DC
+    y = x.copy(); y[: n // 2] = 0; fr.append(y)                       # half silence
+    return np.stack(fr)
+
+
+@pytest.mark.parametrize("n", [256, 512, 1024, 2048])
+def test_nonfinite_and_extreme_frames(capi, oracle_mod, n):
+    x = edge_frames(n)
+    ref = oracle_mod.extract(x)
+    out = capi.Plan(buffer_size=n, scalar_f64=True).extract(x, FEATS)
+    assert np.array_equal(out["zcr"], ref["scalars"][:, 2])
+    compare(out, ref, n)
+
+
+@pytest.mark.parametrize("sr", [8000.0, 22050.0, 48000.0, 96000.0])
+def test_sample_rates(capi, oracle_mod, sr):
+    n = 1024
+    x = oracle_mod.synth_frames(0x6D657964, 77, 48, n)
+    t = np.arange(n) / sr
+    x[::4] = (0.5 * np.sin(2 * np.pi * 1000.0 * t)).astype(np.float32)
+    ref = oracle_mod.extract(x, sample_rate=sr)
+    out = capi.Plan(buffer_size=n, sample_rate=sr, scalar_f64=True).extract(x, FEATS)
+    compare(out, ref, n, sr=sr)
+
+
+@pytest.mark.parametrize("nmel", [1, 7, 16, 17, 26, 33, 40, 64])
+def test_mel_band_counts(capi, oracle_mod, nmel):
+    n = 1024
+    x = oracle_mod.synth_frames(0x6D657964, 300, 40, n)
+    ref = oracle_mod.extract(x, num_mel=nmel)
+    out = capi.Plan(buffer_size=n, num_mel_bands=nmel, scalar_f64=True).extract(x, ["mfcc", "amplitudeSpectrum"])
+    assert not tolerance.check_vectors(out["mfcc"], ref["mfcc"]), nmel
+
+
+def test_n256_batch(capi, oracle_mod):
+    n = 256
+    x = oracle_mod.synth_frames(0x6D657964, 9, 200, n)
+    ref = oracle_mod.extract(x)
+    out = capi.Plan(buffer_size=n, scalar_f64=True).extract(x, FEATS)
+    compare(out, ref, n, spectra_exact_min=0.999)
+
+
+def test_randomized_plans(capi, oracle_mod):
+    """A seeded sweep over (N, window, sample rate, mel bands, signal type, batch size)."""
+    rng = np.random.default_rng(20261015)
+    for case in range(24):
+        n = int(rng.choice([256, 512, 1024, 2048]))
+        window = str(rng.choice(["hanning", "hamming"]))
+        sr = float(rng.choice([16000.0, 44100.0, 48000.0]))
+        nmel = int(rng.integers(1, 65))
+        F = int(rng.integers(1, 70))
+        kind = case % 4
+        t = np.arange(n) / sr
+        if kind == 0:
+            x = rng.uniform(-1, 1, (F, n)).astype(np.float32)
+        elif kind == 1:
+            f = rng.uniform(20, sr / 2, (F, 1))
+            x = (rng.uniform(0.01, 1, (F, 1)) * np.sin(2 * np.pi * f * t)).astype(np.float32)
+        elif kind == 2:
+            x = (rng.standard_normal((F, n)) * 10.0 ** rng.uniform(-8, 3, (F, 1))).astype(np.float32)
+        else:
+            x = np.round(rng.uniform(-1, 1, (F, n)) * 32768) / 32768  # int16-like PCM
+            x = x.astype(np.float32)
+        ref = oracle_mod.extract(x, sample_rate=sr, window=window, num_mel=nmel)
+        out = capi.Plan(buffer_size=n, sample_rate=sr, window=window, num_mel_bands=nmel,
+                        scalar_f64=True).extract(x, FEATS)
+        try:
+            compare(out, ref, n, sr=sr)
+        except AssertionError as e:
+            raise AssertionError("case %d: n=%d window=%s sr=%g nmel=%d F=%d kind=%d: %s"
+                                 % (case, n, window, sr, nmel, F, kind, e))
