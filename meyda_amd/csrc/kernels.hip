@@ -745,8 +745,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // five sums over the lanes. Up to N = 512 (5+ waves per SIMD) they go through one LDS
   // transpose: lane l writes column l of a 5 x 64 table; after the prefix scan, lanes
   // 0..39 each add 8 entries (stride 8) of one row and 3 DPP steps finish the row in
-  // 8-lane groups. At N >= 1024 (4 waves per SIMD) the LDS round trip measured slower
-  // than five DPP wave sums, which are used there.
+  // 8-lane groups; the table is read back at the end of the frame (after the mel sums).
+  // Used up to N = 512 (5+ waves per SIMD); at N >= 1024 five DPP wave sums measured faster.
   constexpr bool kMomLds = N <= 512;
   const double bb = (double)(R * lane), b2 = bb * bb, b3 = b2 * bb, b4 = b3 * bb;
   const double P1 = __builtin_fma(bb, T0, T1);
@@ -775,16 +775,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     pk += (double)av[jj];
   }
   const int roll_m = (total > thr) ? cnt - 1 : L;
-  if constexpr (kMomLds) {
-    wave_sync();
-    const int row = lane < 40 ? lane >> 3 : 0;
-    const double* src = mom + row * 64 + (lane & 7);  // entries g, g+8, ..., g+56: conflict-free
-    double t = ((src[0] + src[8]) + (src[16] + src[24])) + ((src[32] + src[40]) + (src[48] + src[56]));
-    t += dpp_d<0xB1>(t);   // quad_perm [1,0,3,2]
-    t += dpp_d<0x4E>(t);   // quad_perm [2,3,0,1]
-    t += dpp_d<0x141>(t);  // row_half_mirror: each 8-lane group holds its row's total
-    if (lane < 40 && (lane & 7) == 0) (&rec.S[1])[row] = t;  // S[1..4], then ln2sum
-  } else {
+  if constexpr (!kMomLds) {
     const double S1 = wave_sum(P1), S2 = wave_sum(P2), S3 = wave_sum(P3), S4 = wave_sum(P4);
     const double l2 = wave_sum((double)l2f);
     wave_sync();
@@ -811,6 +802,16 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
   } else if (ABL_ON(MELSCAN) && ap->need_mfcc) {
     mel_energies<N>(ap, av, lane, buf, rec);
+  }
+  if constexpr (kMomLds) {
+    wave_sync();
+    const int row = lane < 40 ? lane >> 3 : 0;
+    const double* src = mom + row * 64 + (lane & 7);  // entries g, g+8, ..., g+56: conflict-free
+    double t = ((src[0] + src[8]) + (src[16] + src[24])) + ((src[32] + src[40]) + (src[48] + src[56]));
+    t += dpp_d<0xB1>(t);   // quad_perm [1,0,3,2]
+    t += dpp_d<0x4E>(t);   // quad_perm [2,3,0,1]
+    t += dpp_d<0x141>(t);  // row_half_mirror: each 8-lane group holds its row's total
+    if (lane < 40 && (lane & 7) == 0) (&rec.S[1])[row] = t;  // S[1..4], then ln2sum
   }
 #endif
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
