@@ -34,6 +34,7 @@ typedef const __attribute__((address_space(1))) double2* GTw;
 typedef const __attribute__((address_space(1))) float2* GTwf;
 typedef const __attribute__((address_space(1))) double* GD;
 typedef const __attribute__((address_space(1))) float* GF;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr double kS = 0.7071067811865476;  // Math.SQRT1_2 (lib/jsfft/fft.js:10)
 constexpr float kSf = 0.70710677f;
@@ -606,17 +607,36 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 
   // rms.js / energy.js: sum of squares; zcr.js: sign changes of adjacent samples,
   // `x >= 0` vs `x < 0` (so -0 is non-negative and NaN never counts).
-  float e32 = 0.0f;
+  // Sum of squares as packed float32 FMAs over pairs of chunks; zcr from one ballot per
+  // chunk (x < 0): without NaN samples, x >= 0 is its complement. A NaN sample makes that
+  // lane's sum of squares NaN, and such frames count with both comparisons.
+  f32x2 e2 = {0.0f, 0.0f};
+#pragma unroll
+  for (int c = 0; c < CH; c += 2) {
+    const f32x2 xv = {x[c], x[c + 1]};
+    e2 = __builtin_elementwise_fma(xv, xv, e2);
+  }
+  const float e32 = e2.x + e2.y;
   int z = 0;
   uint64_t pge = 0, plt = 0;
+  if (__ballot(e32 != e32)) {
 #pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    e32 = __builtin_fmaf(x[c], x[c], e32);
-    const uint64_t g = __ballot(x[c] >= 0.0f), l = __ballot(x[c] < 0.0f);
-    z += __popcll(((g & (l >> 1)) | (l & (g >> 1))) & 0x7FFFFFFFFFFFFFFFull);
-    if (c > 0) z += (int)((((pge >> 63) & l) | ((plt >> 63) & g)) & 1ull);
-    pge = g;
-    plt = l;
+    for (int c = 0; c < CH; ++c) {
+      const uint64_t g = __ballot(x[c] >= 0.0f), l = __ballot(x[c] < 0.0f);
+      z += __popcll(((g & (l >> 1)) | (l & (g >> 1))) & 0x7FFFFFFFFFFFFFFFull);
+      if (c > 0) z += (int)((((pge >> 63) & l) | ((plt >> 63) & g)) & 1ull);
+      pge = g;
+      plt = l;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const uint64_t l = __ballot(x[c] < 0.0f), g = ~l;
+      z += __popcll(((g & (l >> 1)) | (l & (g >> 1))) & 0x7FFFFFFFFFFFFFFFull);
+      if (c > 0) z += (int)((((pge >> 63) & l) | ((plt >> 63) & g)) & 1ull);
+      pge = g;
+      plt = l;
+    }
   }
   // float32 partial sums are within 1e-6 relative of the double sum; a wave whose
   // partials leave [2^-100, 2^100] (silence, denormal or huge input) redoes it in double.
@@ -640,7 +660,12 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   {
     const GF w = gbl(ap->t.window);
 #pragma unroll
-    for (int c = 0; c < CH; ++c) x[c] *= w[c * 64 + lane];
+    for (int c = 0; c < CH; c += 2) {  // packed float32 multiplies
+      const f32x2 xv = {x[c], x[c + 1]}, wv = {w[c * 64 + lane], w[(c + 1) * 64 + lane]};
+      const f32x2 y = xv * wv;
+      x[c] = y.x;
+      x[c + 1] = y.y;
+    }
   }
   if constexpr (LITERAL) {
     // The snapshot never transforms per buffer: |w x| is the "spectrum".
