@@ -143,6 +143,19 @@ __device__ __forceinline__ double2 ld_tw(GTw p, int i) {
   const GD q = (GD)p;
   return make_double2(q[2 * i], q[2 * i + 1]);
 }
+// A twiddle whose index is the same on every lane (pass 0, and every block-start pair):
+// read through the constant address space, so it is an s_load into SGPRs (scalar cache)
+// instead of a vector load through the texture path, and costs no VGPRs.
+typedef const __attribute__((address_space(4))) double* CD;
+typedef const __attribute__((address_space(4))) float* CF;
+__device__ __forceinline__ double2 ld_tw_u(GTw p, int i) {
+  const CD q = (CD)(uintptr_t)p;
+  return make_double2(q[2 * i], q[2 * i + 1]);
+}
+__device__ __forceinline__ float2 ld_twf_u(GTwf p, int i) {
+  const CF q = (CF)(uintptr_t)p;
+  return make_float2(q[2 * i], q[2 * i + 1]);
+}
 __device__ __forceinline__ float2 ld_twf(GTwf p, int i) {
   const GF q = (GF)p;
   return make_float2(q[2 * i], q[2 * i + 1]);
@@ -156,10 +169,10 @@ __device__ __forceinline__ float2 ld_twf(GTwf p, int i) {
 //
 // Generic pair:      lo <- s L + c R,   hi <- conj(s L - c R)
 // Block-start pair:  exactly jsfft's operations for j = 0 and j = w/2.
-template <bool FAITH>
+template <bool FAITH, bool UNI = false>
 __device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, GTw tw, GTwf twf, int idx) {
   if constexpr (FAITH) {
-    const double2 c = ld_tw(tw, idx);
+    const double2 c = UNI ? ld_tw_u(tw, idx) : ld_tw(tw, idx);
     const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
     const double Ar = __builtin_fma(c.x, Rr, -(c.y * Ri));
     const double Ai = __builtin_fma(c.x, Ri, c.y * Rr);
@@ -168,7 +181,7 @@ __device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, GTw tw, GTw
     hi.x = (float)__builtin_fma(kS, Lr, -Ar);
     hi.y = (float)__builtin_fma(-kS, Li, Ai);
   } else {
-    const float2 c = ld_twf(twf, idx);
+    const float2 c = UNI ? ld_twf_u(twf, idx) : ld_twf(twf, idx);
     const float Ar = __builtin_fmaf(c.x, hi.x, -(c.y * hi.y));
     const float Ai = __builtin_fmaf(c.x, hi.y, c.y * hi.x);
     const float Lr = lo.x, Li = lo.y;
@@ -182,14 +195,14 @@ __device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, GTw tw, GTw
 template <bool FAITH>
 __device__ __forceinline__ void bfly_special(float2& lo, float2& hi, GTw tw, GTwf twf, int idx) {
   if constexpr (FAITH) {
-    const double2 f = ld_tw(tw, idx);
+    const double2 f = ld_tw_u(tw, idx);
     const double L0 = lo.x, Lh = lo.y, R0 = hi.x, Rh = hi.y;
     lo.x = (float)(kS * (L0 + R0));
     lo.y = (float)(kS * (L0 - R0));
     hi.x = (float)(kS * (Lh + f.x * Rh));
     hi.y = (float)(kS * (f.y * Rh));
   } else {
-    const float2 f = ld_twf(twf, idx);
+    const float2 f = ld_twf_u(twf, idx);
     const float L0 = lo.x, Lh = lo.y, R0 = hi.x, Rh = hi.y;
     lo.x = kSf * (L0 + R0);
     lo.y = kSf * (L0 - R0);
@@ -206,7 +219,7 @@ template <bool FAITH>
 __device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf twf, int idx, int fidx, bool sp) {
   if constexpr (FAITH) {
     const double2 c = ld_tw(tw, idx);
-    const double2 f = ld_tw(tw, fidx);
+    const double2 f = ld_tw_u(tw, fidx);
     const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
     const double Ar = __builtin_fma(c.x, Rr, -(c.y * Ri));
     const double Ai = __builtin_fma(c.x, Ri, c.y * Rr);
@@ -220,7 +233,7 @@ __device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf 
     hi.y = (float)(sp ? s3 : g3);
   } else {
     const float2 c = ld_twf(twf, idx);
-    const float2 f = ld_twf(twf, fidx);
+    const float2 f = ld_twf_u(twf, fidx);
     const float Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
     const float Ar = __builtin_fmaf(c.x, Rr, -(c.y * Ri));
     const float Ai = __builtin_fmaf(c.x, Ri, c.y * Rr);
@@ -251,7 +264,7 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
     const int hi = r | (1 << I);
     if constexpr (P == 0) {
       if (rp == 0) bfly_special<FAITH>(v[r], v[hi], tw, twf, fidx);
-      else bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + rp);
+      else bfly_generic<FAITH, true>(v[r], v[hi], tw, twf, mask + rp);
 #ifndef MGX_ABL_BRANCH
     } else if (rp == 0) {
       bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, fidx, la == 0);
@@ -941,7 +954,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // frame, then phase 2 over the batch, with wave-level synchronisation only.
   const uint64_t nf = ap->num_frames;
   const uint64_t nb = (nf + FPW - 1) / FPW;
+#ifdef MGX_ABL_GRIDSTRIDE
   const uint64_t wstride = (uint64_t)gridDim.x * 4;
+  const uint64_t b0 = (uint64_t)blockIdx.x * 4 + wave, bend = nb;
+#else
+  // Each workgroup owns one contiguous range of batches, its 4 waves interleaved
+  // (wave w takes batches 4k + w), so the 16 frames the waves finish together are
+  // consecutive: a workgroup fills whole 64/128-byte lines of every scalar output in its
+  // own XCD's L2 instead of sharing each line with a workgroup on another XCD.
+  const uint64_t wstride = 4;
+  const uint64_t ng = (nb + 3) / 4, per = (ng + gridDim.x - 1) / gridDim.x;
+  const uint64_t g0 = (uint64_t)blockIdx.x * per, g1 = g0 + per < ng ? g0 + per : ng;
+  const uint64_t b0 = g0 * 4 + wave, bend = g1 * 4 < nb ? g1 * 4 : nb;
+#endif
   // Register prefetch: the next frame of this wave is loaded while this one is processed.
   // Loads are unconditional (the frame index is clamped; results of frames past the end
   // are never stored), so they issue back to back with no branches or waits between them.
@@ -953,10 +978,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     for (int c = 0; c < CH; ++c) xv[c] = xin[c * 64 + lane];
   };
   float xn[CH];
-  const uint64_t b0 = (uint64_t)blockIdx.x * 4 + wave;
   load(xn, b0, 0);
 
-  for (uint64_t b = b0; b < nb; b += wstride) {
+  for (uint64_t b = b0; b < bend; b += wstride) {
     const uint64_t f0 = b * FPW;
     // ------------------------------------------------------------- phase 1
     for (int j = 0; j < FPW; ++j) {
