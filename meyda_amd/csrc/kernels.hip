@@ -85,6 +85,15 @@ struct Geo {
   static constexpr int WPE = N <= 1024 ? 4 : 2;
   // exchange layout (phys) needs L + L/16 + 2 slots (also >= the L-double prefix row)
   static constexpr int SLOT_PHYS = L + (L >> 4) + 2;
+  // Moment sums through an LDS transpose (5 rows of 64 doubles per wave, row stride 72 so
+  // the rows read together fall in different banks) rather than 5 DPP wave sums: measured
+  // faster up to N = 1024 (4+ waves per SIMD), slower at 2048 (2 waves).
+#ifdef MGX_ABL_MOMDPP
+  static constexpr bool MOM_LDS = N <= 512;
+#else
+  static constexpr bool MOM_LDS = N <= 1024;
+#endif
+  static constexpr int MOM_STRIDE = 72;
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
 
@@ -227,10 +236,15 @@ __device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf 
     const double g2 = __builtin_fma(kS, Lr, -Ar), g3 = __builtin_fma(-kS, Li, Ai);
     const double s0 = kS * (Lr + Rr), s1 = kS * (Lr - Rr);
     const double s2 = kS * (Li + f.x * Ri), s3 = kS * (f.y * Ri);
+#ifdef MGX_ABL_MIXGEN
+    lo.x = (float)g0; lo.y = (float)g1; hi.x = (float)g2; hi.y = (float)g3;
+    (void)s0; (void)s1; (void)s2; (void)s3; (void)sp;
+#else
     lo.x = (float)(sp ? s0 : g0);
     lo.y = (float)(sp ? s1 : g1);
     hi.x = (float)(sp ? s2 : g2);
     hi.y = (float)(sp ? s3 : g3);
+#endif
   } else {
     const float2 c = ld_twf(twf, idx);
     const float2 f = ld_twf_u(twf, fidx);
@@ -363,7 +377,11 @@ __device__ __forceinline__ double wave_inclusive_scan(double v) {
 // Amplitude of one slot: src/meyda.js:104-114, sqrt(re^2 + im^2) in double, stored to float32.
 template <bool FAITH>
 __device__ __forceinline__ float slot_amp(float re, float im) {
+#ifdef MGX_ABL_AMP32
+  if constexpr (false) {
+#else
   if constexpr (FAITH) {
+#endif
     // s = re^2 + im^2 lies in [2^-298, 2^256) or is 0/inf/NaN, so the library sqrt's
     // range scaling is not needed: rsq seed + the two-residual refinement (full double
     // accuracy), then 0/inf/NaN pass through.
@@ -458,7 +476,7 @@ struct Lds {
   static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2 + 64) * 4, "mel scratch must fit");
   // Per wave, the 5 x 64 table of moment partials (transposed reduction, N <= 512).
   static constexpr size_t mom_off = slot_off + slot_bytes;
-  static constexpr size_t mom_bytes = N <= 512 ? (size_t)4 * 5 * 64 * 8 : 0;
+  static constexpr size_t mom_bytes = G::MOM_LDS ? (size_t)4 * 5 * G::MOM_STRIDE * 8 : 0;
   // Frame records: FPW per wave.
   static constexpr size_t rec_off = mom_off + mom_bytes;
   // The DCT table (mfcc.js:67-83), staged once per workgroup, sized per plan.
@@ -775,28 +793,36 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       T3 = __builtin_fma((double)(jj * jj * jj), ad, T3);
       T4 = __builtin_fma((double)(jj * jj * jj * jj), ad, T4);
     }
-    l2f += log2f(av[jj]);
+    l2f += __builtin_amdgcn_logf(av[jj]);  // the bare v_log_f32: == log2f for normal inputs
+  }
+  // v_log_f32 flushes a denormal input to 0 (-inf). A wave whose sum is not finite (a
+  // zero, denormal, infinite or NaN amplitude; rare) recomputes with log2f's scaling.
+  if (__ballot(!(__builtin_fabsf(l2f) < __builtin_huge_valf()))) {
+    l2f = 0.0f;
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) l2f += log2f(av[jj]);
   }
   wave_sync();  // every lane has read the amplitude row: the buffer takes the prefix sums next
   FrameRec& rec = recs[fb];
   // Moments S1..S4 (bin-offset polynomial shift of the local partials) and sum log2 a:
-  // five sums over the lanes. Up to N = 512 (5+ waves per SIMD) they go through one LDS
-  // transpose: lane l writes column l of a 5 x 64 table; after the prefix scan, lanes
-  // 0..39 each add 8 entries (stride 8) of one row and 3 DPP steps finish the row in
-  // 8-lane groups; the table is read back at the end of the frame (after the mel sums).
-  // Used up to N = 512 (5+ waves per SIMD); at N >= 1024 five DPP wave sums measured faster.
-  constexpr bool kMomLds = N <= 512;
+  // five sums over the lanes. Up to N = 1024 they go through one LDS transpose: lane l
+  // writes column l of a 5 x 64 table; after the prefix scan, lanes 0..39 each add 8
+  // entries (stride 8) of one row and 3 DPP steps finish the row in 8-lane groups; the
+  // table is read back at the end of the frame (after the mel sums). At N = 2048 (2 waves
+  // per SIMD) five DPP wave sums measured faster.
+  constexpr bool kMomLds = G::MOM_LDS;
+  constexpr int MS = G::MOM_STRIDE;
   const double bb = (double)(R * lane), b2 = bb * bb, b3 = b2 * bb, b4 = b3 * bb;
   const double P1 = __builtin_fma(bb, T0, T1);
   const double P2 = T2 + 2.0 * bb * T1 + b2 * T0;
   const double P3 = T3 + 3.0 * bb * T2 + 3.0 * b2 * T1 + b3 * T0;
   const double P4 = T4 + 4.0 * bb * T3 + 6.0 * b2 * T2 + 4.0 * b3 * T1 + b4 * T0;
   if constexpr (kMomLds) {
-    mom[0 * 64 + lane] = P1;
-    mom[1 * 64 + lane] = P2;
-    mom[2 * 64 + lane] = P3;
-    mom[3 * 64 + lane] = P4;
-    mom[4 * 64 + lane] = (double)l2f;
+    mom[0 * MS + lane] = P1;
+    mom[1 * MS + lane] = P2;
+    mom[2 * MS + lane] = P3;
+    mom[3 * MS + lane] = P4;
+    mom[4 * MS + lane] = (double)l2f;
   }
   // prefix P(k) = sum_{i<k} a_i: lane-exclusive offset + local prefix
   const double incl = wave_inclusive_scan(T0);
@@ -814,8 +840,13 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
   const int roll_m = (total > thr) ? cnt - 1 : L;
   if constexpr (!kMomLds) {
+#ifdef MGX_ABL_NOWSUM
+    const double S1 = readlane_d(P1, 63), S2 = readlane_d(P2, 63), S3 = readlane_d(P3, 63), S4 = readlane_d(P4, 63);
+    const double l2 = readlane_d((double)l2f, 63);
+#else
     const double S1 = wave_sum(P1), S2 = wave_sum(P2), S3 = wave_sum(P3), S4 = wave_sum(P4);
     const double l2 = wave_sum((double)l2f);
+#endif
     wave_sync();
     if (lane == 0) {
       rec.S[1] = S1; rec.S[2] = S2; rec.S[3] = S3; rec.S[4] = S4;
@@ -844,7 +875,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   if constexpr (kMomLds) {
     wave_sync();
     const int row = lane < 40 ? lane >> 3 : 0;
-    const double* src = mom + row * 64 + (lane & 7);  // entries g, g+8, ..., g+56: conflict-free
+    const double* src = mom + row * MS + (lane & 7);  // entries g, g+8, ..., g+56 of the row
     double t = ((src[0] + src[8]) + (src[16] + src[24])) + ((src[32] + src[40]) + (src[48] + src[56]));
     t += dpp_d<0xB1>(t);   // quad_perm [1,0,3,2]
     t += dpp_d<0x4E>(t);   // quad_perm [2,3,0,1]
@@ -923,7 +954,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
   float* dct_lds = reinterpret_cast<float*>(smem + LY::dct_off);
-  double* mom = reinterpret_cast<double*>(smem + LY::mom_off) + (threadIdx.x >> 6) * (5 * 64);
+  double* mom = reinterpret_cast<double*>(smem + LY::mom_off) + (threadIdx.x >> 6) * (5 * G::MOM_STRIDE);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
