@@ -65,6 +65,19 @@ constexpr int rev_bits(int x, int bits) {
   return r;
 }
 
+// Padded slot address of an FFT exchange: loc + sum k (loc >> s), additive over the
+// disjoint lane and register bits of a location, so phys(lane part) + phys(register part)
+// (the register part an immediate offset). Chosen per N by a search over the LDS bank
+// rule of ds_write2_b64 / ds_read2_b64 (4 groups of 16 lanes, banks (a/4) mod 32): the
+// exchanges then take the conflict-free minimum of LDS cycles at N = 512, 1024 and 2048.
+template <int N>
+__host__ __device__ constexpr int phys(int loc) {
+  return N == 256 ? loc + 2 * (loc >> 4) + (loc >> 6)
+       : N == 512 ? loc + 4 * (loc >> 4) + (loc >> 6)
+       : N == 1024 ? loc + 2 * (loc >> 4) + (loc >> 7)
+       : loc + (loc >> 6);
+}
+
 template <int N>
 struct Geo {
   static constexpr int L = N / 2;           // slots per frame == amplitude bins
@@ -83,8 +96,11 @@ struct Geo {
   // allows 4 workgroups per CU; 2 waves (<= 256) at N = 2048. Without the bound the
   // allocator drifts past the threshold (129 VGPRs, or 251 + 32 AGPRs) and occupancy halves.
   static constexpr int WPE = N <= 1024 ? 4 : 2;
-  // exchange layout (phys) needs L + L/16 + 2 slots (also >= the L-double prefix row)
-  static constexpr int SLOT_PHYS = L + (L >> 4) + 2;
+  // Slot buffer entries (8 bytes): the padded exchange image, the natural-order half
+  // spectrum X[0..L] (complex output), the padded prefix row (pd) and the mel scratch.
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int SLOT_PHYS =
+      cmax(cmax(phys<N>(L - 1) + 1, L + 1), cmax(L + 2 * (L >> 5) + 1, 2 * (kMaxMel + 2 + 64) * 4 / 8));
   // Moment sums through an LDS transpose (5 rows of 64 doubles per wave, row stride 72 so
   // the rows read together fall in different banks) rather than 5 DPP wave sums: measured
   // faster up to N = 1024 (4+ waves per SIMD), slower at 2048 (2 waves).
@@ -130,7 +146,13 @@ struct PassGeo {
   }
 };
 
-__device__ __forceinline__ int phys(int loc) { return loc + (loc >> 4); }
+
+// Bank-padded layouts of the amplitude row (floats) and of its prefix sums (doubles) in
+// the slot buffer: lane l reads/writes R consecutive entries with 16-byte accesses, and
+// 4 floats (2 doubles) of padding per 64 floats (32 doubles) shift each successive group
+// of lanes onto the banks the previous group left free (no 2- or 4-way conflicts).
+__device__ __forceinline__ int pa(int k) { return k + 4 * (k >> 6); }
+__device__ __forceinline__ int pd(int d) { return d + 2 * (d >> 5); }
 
 
 // Wave-level LDS ordering (no global-memory fence: in-flight prefetch loads stay in flight).
@@ -315,13 +337,13 @@ template <int N, int P>
 __device__ __forceinline__ void exchange(float2 (&v)[Geo<N>::R], int lp_prev, int lp_cur, float2* buf) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
-  const int bprev = phys(lp_prev), bcur = phys(lp_cur);
+  const int bprev = phys<N>(lp_prev), bcur = phys<N>(lp_cur);
   wave_sync();
 #pragma unroll
-  for (int r = 0; r < G::R; ++r) buf[bprev + phys(PG::rpart(P - 1, r))] = v[r];
+  for (int r = 0; r < G::R; ++r) buf[bprev + phys<N>(PG::rpart(P - 1, r))] = v[r];
   wave_sync();
 #pragma unroll
-  for (int r = 0; r < G::R; ++r) v[r] = buf[bcur + phys(PG::rpart(P, r))];
+  for (int r = 0; r < G::R; ++r) v[r] = buf[bcur + phys<N>(PG::rpart(P, r))];
 }
 
 template <int N, int P, bool FAITH>
@@ -701,7 +723,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   if constexpr (LITERAL) {
     // The snapshot never transforms per buffer: |w x| is the "spectrum".
 #pragma unroll
-    for (int c = 0; c < R; ++c) amp[c * 64 + lane] = fabsf(x[c]);
+    for (int c = 0; c < R; ++c) amp[pa(c * 64 + lane)] = fabsf(x[c]);
   } else {
     // Stage 0 (jsfft width 1) at load: slot j = rev(e) pairs x[e] with x[e + N/2].
     float2 v[R];
@@ -741,7 +763,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
           buf[0] = make_float2(v[r].x, 0.0f);
           buf[L] = make_float2(v[r].y, 0.0f);
         } else {
-          buf[kl[r]] = v[r];
+          buf[kl[r] - 4 * (kl[r] / 68)] = v[r];  // kl holds pa(bin)
         }
       }
       wave_sync();
@@ -758,20 +780,20 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       wave_sync();
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) amp[kl[r]] = ar[r];
+    for (int r = 0; r < R; ++r) amp[kl[r]] = ar[r];  // kl[r] = pa(bin)
   }
   wave_sync();
 
   if (valid && ap->out.amplitude_spectrum) {
     auto o = gbl(ap->out.amplitude_spectrum) + f * (uint64_t)L;
 #pragma unroll
-    for (int c = 0; c < R; ++c) o[c * 64 + lane] = amp[c * 64 + lane];
+    for (int c = 0; c < R; ++c) o[c * 64 + lane] = amp[pa(c * 64 + lane)];
   }
   if (valid && ap->out.power_spectrum) {
     auto o = gbl(ap->out.power_spectrum) + f * (uint64_t)L;
 #pragma unroll
     for (int c = 0; c < R; ++c) {
-      const float av = amp[c * 64 + lane];
+      const float av = amp[pa(c * 64 + lane)];
       o[c * 64 + lane] = av * av;  // powerSpectrum.js
     }
   }
@@ -780,7 +802,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // Per-frame reductions, lane t owns bins [R t, R t + R).
   float av[R];
 #pragma unroll
-  for (int jj = 0; jj < R; ++jj) av[jj] = amp[R * lane + jj];
+  for (int jj = 0; jj < R; ++jj) av[jj] = amp[pa(R * lane + jj)];
   double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
   float l2f = 0.0f;
 #pragma unroll
@@ -834,7 +856,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   double pk = excl;  // P(R lane + jj), accumulated again rather than kept (registers)
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) {
-    pbuf[R * lane + jj] = pk;
+    pbuf[pd(R * lane + jj)] = pk;
     cnt += __popcll(__ballot(pk <= thr));
     pk += (double)av[jj];
   }
@@ -855,7 +877,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
   if (lane < kBark) {
     const auto lim = gbl(ap->t.bblim);
-    rec.band[lane] = pbuf[lim[lane + 1]] - pbuf[lim[lane]];
+    rec.band[lane] = pbuf[pd(lim[lane + 1])] - pbuf[pd(lim[lane])];
   }
   if (lane == 0) {
     rec.S[0] = total;
@@ -977,7 +999,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   {
     const auto klist = gbl(ap->t.klist);
 #pragma unroll
-    for (int r = 0; r < R; ++r) kl[r] = klist[lp[G::NPASS - 1] | PG::rpart(G::NPASS - 1, r)];
+    for (int r = 0; r < R; ++r) kl[r] = pa(klist[lp[G::NPASS - 1] | PG::rpart(G::NPASS - 1, r)]);
   }
   const bool dc_lane = lp[G::NPASS - 1] == 0;
 

@@ -5,7 +5,8 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd /tmp && export TMPDIR=/tmp
 for v in "$@"; do
   if [ $v = base ]; then unset MEYDA_AMD_LIB; else export MEYDA_AMD_LIB=$R/abl/libabl_$v.so; fi
-  for set in ${PMC_SETS:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_FMA_F64"}; do
+  IFS='|' read -ra SETS <<< "${PMC_SETS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS|SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES|SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_FMA_F64}"
+  for set in "${SETS[@]}"; do
     tag=$(echo $set | tr ' ' '_' | cut -c1-40)
     timeout -k 10 120 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $R/gpurun_out/pmc/$v/$tag -o run -- python3 $R/tools/pmc_probe.py > /dev/null 2>&1 || { echo "pmc failed $v $set"; exit 1; }
   done
