@@ -444,7 +444,8 @@ __device__ __forceinline__ float pow023(double x) {
   int e;
   const double m = 2.0 * frexp(x, &e);  // [1, 2)
   const float mh = (float)m, ml = (float)(m - (double)mh);
-  const float l2m = __builtin_fmaf(ml, 1.4426950408889634f / mh, __builtin_amdgcn_logf(mh));
+  // (the correction ml / (mh ln 2) is ~2^-24 relative: a hardware reciprocal suffices)
+  const float l2m = __builtin_fmaf(ml * 1.4426950408889634f, __builtin_amdgcn_rcpf(mh), __builtin_amdgcn_logf(mh));
   const double y = 0.23 * ((double)(e - 1) + (double)l2m);
   const double n = floor(y);
   return ldexpf(__builtin_amdgcn_exp2f((float)(y - n)), (int)n);
@@ -927,6 +928,15 @@ __device__ __forceinline__ double dct_sum(const float* dct, const float* lm, int
   return v;
 }
 
+// 2^y in double for the geometric mean of spectralFlatness.js: 2^floor(y) * 2^frac(y) with
+// the f32 hardware exp2 on [0, 1) (relative error ~1.5e-7, against the 1e-5 bar); |y|
+// beyond the f32 exponent range (a zero amplitude makes y = -inf) takes the library exp2.
+__device__ __forceinline__ double exp2_mean(double y) {
+  if (!(__builtin_fabs(y) < 1000.0)) return exp2(y);
+  const double n = floor(y);
+  return ldexp((double)__builtin_amdgcn_exp2f((float)(y - n)), (int)n);
+}
+
 // One of the ten spectral/time scalars of a frame from its phase-1 record, formulas as
 // written in the reference extractors. Branch-free: every lane evaluates the shared terms
 // (moments, spread) and selects its feature's numerator and denominator, so a wave
@@ -935,8 +945,10 @@ template <int N>
 __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int sc) {
   constexpr int L = N / 2;
   const double S0 = rc.S[0];
-  // utils.js:1-11 mu(p) = sum k^p a_k / sum a_k
-  const double m1 = rc.S[1] / S0, m2 = rc.S[2] / S0, m3 = rc.S[3] / S0, m4 = rc.S[4] / S0;
+  // utils.js:1-11 mu(p) = sum k^p a_k / sum a_k: one reciprocal and four products (S0 is
+  // 0, >= 2^-149 or non-finite, so 1/S0 neither overflows nor hides a NaN of the quotient)
+  const double inv = 1.0 / S0;
+  const double m1 = rc.S[1] * inv, m2 = rc.S[2] * inv, m3 = rc.S[3] * inv, m4 = rc.S[4] * inv;
   const double sd = sqrt(m2 - m1 * m1);  // spectralSpread.js
   double num, den = 1.0;
   switch (sc) {  // selects only (no divergent code: every case is a few operands)
@@ -945,7 +957,7 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
     case MGX_ZCR: num = (double)rc.zcr; break;         // zcr.js
     case MGX_SPECTRAL_CENTROID: num = m1; break;       // spectralCentroid.js
     case MGX_SPECTRAL_FLATNESS:                        // spectralFlatness.js: geometric / arithmetic mean
-      num = exp(rc.ln2sum * kLn2 / L) * L;
+      num = exp2_mean(rc.ln2sum * (1.0 / L)) * L;
       den = S0;
       break;
     case MGX_SPECTRAL_SLOPE:                           // spectralSlope.js:9-21
