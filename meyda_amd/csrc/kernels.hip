@@ -1121,12 +1121,51 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       const int l2 = opaque(lane);
       if (ABL_ON(DCT) && q->need_spectrum && q->need_mfcc) {
         const int nc = q->ncoef, nfilt = q->nfilt;
+#ifndef MGX_DCT_MFMA
+        // VALU: one lane per (coefficient, frame). (The MFMA form below measured 2 % slower
+        // for the whole kernel at N = 1024: DESIGN.md §4.2.)
         for (int i = l2; i < FPW * nc; i += 64) {
           const int c = i / FPW, fb = i % FPW;
           const uint64_t f = f0 + fb;
           const double v = dct_sum(dct_lds, recs[fb].lm, c, nc, nfilt);
           if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(v / nc);
         }
+#else
+        // mfcc.js:85-93 as a dense contraction on the matrix cores: D[c][f] = sum_n
+        // dct[c][n] lm_f[n] with v_mfma_f64_16x16x4_f64 (A = DCT rows, B = the batch's
+        // log-mel columns, K = 4 bands per step). Products of two floats are exact in
+        // double, as in the reference; only the order of the f64 sum differs (~1e-16).
+        // Lane l: A[c = l & 15][k = l >> 4], B[k = l >> 4][f = l & 15];
+        // D: f = l & 15, c = (l >> 4) + 4 r (r = 0..3).
+        static_assert(FPW <= 16, "one MFMA column per frame of the batch");
+        const int col = l2 & 15, krow = l2 >> 4, ks = (nfilt + 3) >> 2;
+        const float* lmcol = recs[col < FPW ? col : 0].lm;
+        for (int mt = 0; mt < nc; mt += 16) {
+          typedef double f64x4 __attribute__((ext_vector_type(4)));
+          // two independent accumulation chains (even / odd steps; the tables are padded
+          // to 8 bands, so the steps come in pairs) halve the MFMA dependency latency
+          f64x4 acc = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+          const int ca = mt + col;
+          for (int st = 0; st < ks; st += 2) {
+            const int n = 4 * st + krow;  // < nfilt rounded up to 8: tables are zero-padded
+            const float av0 = ca < nc ? dct_lds[ca + n * nc] : 0.0f;
+            const float bv0 = col < FPW ? lmcol[n] : 0.0f;
+            const float av1 = ca < nc ? dct_lds[ca + (n + 4) * nc] : 0.0f;
+            const float bv1 = col < FPW ? lmcol[n + 4] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)av0, (double)bv0, acc, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)av1, (double)bv1, acc1, 0, 0, 0);
+          }
+          acc += acc1;
+          const uint64_t f = f0 + col;
+          if (col < FPW && f < q->num_frames && q->out.mfcc) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int c = mt + krow + 4 * r;
+              if (c < nc) gbl(q->out.mfcc)[f * nc + c] = (float)(acc[r] / nc);
+            }
+          }
+        }
+#endif
       }
       // the other scalar features: one lane per (feature, frame)
       for (int i = l2; ABL_ON(FIN) && i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {
