@@ -197,7 +197,7 @@ __device__ __forceinline__ float2 ld_twf(GTwf p, int i) {
 // ---------------------------------------------------------------- butterflies
 // Twiddle table of stage q (input blocks of 2^(q+1) samples) at offset 2^q - 1:
 // entry a holds c = SQRT1_2 * f_k(a) for the slot pair (a, a + 2^q) (entry 0: S f_0 =
-// (S, 0)); after the N/2 - 1 stage entries, entry N/2 - 1 + q holds f_{w/2} unscaled
+// (S, 0)); after the N/2 - 1 stage entries, entry N/2 - 1 + q holds S f_{w/2}
 // for the block-start pair, whose slots pack (X[0], X[w/2]).
 //
 // Generic pair:      lo <- s L + c R,   hi <- conj(s L - c R)
@@ -227,20 +227,22 @@ __device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, GTw tw, GTw
 
 template <bool FAITH>
 __device__ __forceinline__ void bfly_special(float2& lo, float2& hi, GTw tw, GTwf twf, int idx) {
+  // f = SQRT1_2 f_{w/2}: S (Lh + f_x Rh) as S Lh + (S f_x) Rh and S (f_y Rh) as (S f_y) Rh
+  // (one f64 rounding moved in each; the exact j = 0 sums S (L0 +- R0) stay as written)
   if constexpr (FAITH) {
     const double2 f = ld_tw_u(tw, idx);
     const double L0 = lo.x, Lh = lo.y, R0 = hi.x, Rh = hi.y;
     lo.x = (float)(kS * (L0 + R0));
     lo.y = (float)(kS * (L0 - R0));
-    hi.x = (float)(kS * (Lh + f.x * Rh));
-    hi.y = (float)(kS * (f.y * Rh));
+    hi.x = (float)__builtin_fma(kS, Lh, f.x * Rh);
+    hi.y = (float)(f.y * Rh);
   } else {
     const float2 f = ld_twf_u(twf, idx);
     const float L0 = lo.x, Lh = lo.y, R0 = hi.x, Rh = hi.y;
     lo.x = kSf * (L0 + R0);
     lo.y = kSf * (L0 - R0);
-    hi.x = kSf * __builtin_fmaf(f.x, Rh, Lh);
-    hi.y = kSf * (f.y * Rh);
+    hi.x = __builtin_fmaf(kSf, Lh, f.x * Rh);
+    hi.y = f.y * Rh;
   }
 }
 
@@ -259,7 +261,7 @@ __device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf 
     const double g0 = __builtin_fma(kS, Lr, Ar), g1 = __builtin_fma(kS, Li, Ai);
     const double g2 = __builtin_fma(kS, Lr, -Ar), g3 = __builtin_fma(-kS, Li, Ai);
     const double s0 = kS * (Lr + Rr), s1 = kS * (Lr - Rr);
-    const double s2 = kS * (Li + f.x * Ri), s3 = kS * (f.y * Ri);
+    const double s2 = __builtin_fma(kS, Li, f.x * Ri), s3 = f.y * Ri;  // f = S f_{w/2}
 #ifdef MGX_ABL_MIXGEN
     lo.x = (float)g0; lo.y = (float)g1; hi.x = (float)g2; hi.y = (float)g3;
     (void)s0; (void)s1; (void)s2; (void)s3; (void)sp;
@@ -278,7 +280,7 @@ __device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf 
     const float g0 = __builtin_fmaf(kSf, Lr, Ar), g1 = __builtin_fmaf(kSf, Li, Ai);
     const float g2 = __builtin_fmaf(kSf, Lr, -Ar), g3 = __builtin_fmaf(-kSf, Li, Ai);
     const float s0 = kSf * (Lr + Rr), s1 = kSf * (Lr - Rr);
-    const float s2 = kSf * __builtin_fmaf(f.x, Ri, Li), s3 = kSf * (f.y * Ri);
+    const float s2 = __builtin_fmaf(kSf, Li, f.x * Ri), s3 = f.y * Ri;
     lo.x = sp ? s0 : g0;
     lo.y = sp ? s1 : g1;
     hi.x = sp ? s2 : g2;
@@ -424,6 +426,25 @@ __device__ __forceinline__ float slot_amp(float re, float im) {
   } else {
     return sqrtf(__builtin_fmaf(re, re, im * im));
   }
+}
+
+// The same amplitude through the f32 hardware reciprocal square root plus one f64 Heron
+// correction (about half the issue cycles: v_rsq_f64 alone costs 16 cycles per wave, the
+// f64 Newton chain 9 more f64 operations). s = re^2 + im^2 exactly as above; q = rsq(s) in
+// f32, y = s q (~2^-22 relative), then g = y + (s - y^2) q / 2 in f64 (~2^-43 relative),
+// rounded to float32: equal to the correctly rounded sqrt unless sqrt(s) lies within 2^-43
+// of a float32 rounding boundary (~2^-19 of the bins; those move by one ulp). ok is false
+// when s leaves [2^-120, 2^120] (0, denormal-range, huge, inf, NaN): the caller then redoes
+// the wave's frame with slot_amp.
+__device__ __forceinline__ float slot_amp_rsq(float re, float im, bool& ok) {
+  const double xr = re, xi = im;
+  const double s = __builtin_fma(xr, xr, xi * xi);
+  const float sf = (float)s;
+  ok = sf >= 0x1p-120f && sf <= 0x1p120f;
+  const float q = __builtin_amdgcn_rsqf(sf);
+  const double y = (double)(sf * q);
+  const double r = __builtin_fma(-y, y, s);
+  return (float)__builtin_fma(r, (double)(0.5f * q), y);
 }
 
 struct FrameRec {
@@ -750,10 +771,30 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     const bool want_cplx = ap->out.complex_real != nullptr;
     // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
     float ar[R];
+#ifndef MGX_ABL_AMP64
+    if constexpr (FAITH) {
+      bool ok = true;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        bool okr;
+        ar[r] = slot_amp_rsq(v[r].x, v[r].y, okr);
+        // (the packed DC/Nyquist slot is replaced below: its range does not matter)
+        if (PG::rpart(G::NPASS - 1, r) == 0) okr = okr || dc_lane;
+        ok = ok && okr;
+      }
+      if (__ballot(!ok)) {  // a zero, tiny, huge or non-finite |X|^2 somewhere in the frame
+#pragma unroll
+        for (int r = 0; r < R; ++r) ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);
+      }
+    } else
+#endif
+    {
+#pragma unroll
+      for (int r = 0; r < R; ++r) ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const bool dc = (PG::rpart(G::NPASS - 1, r) == 0) && dc_lane;
-      ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);
       if (dc) ar[r] = fabsf(v[r].x);  // slot 0 packs (X[0], X[N/2]), both real
     }
     wave_sync();  // the last exchange's reads are done: the slot buffer is free

@@ -117,7 +117,7 @@ void klist(int m, std::vector<int>& k) {
 }
 // lib/jsfft/fft.js:140-165: per stage, f_j by the recurrence from (cos pi/w, sin pi/w).
 // Entry a of stage q (input blocks of w = 2^(q+1) samples, offset 2^q - 1) holds
-// SQRT1_2 * f_{k(a)} (a = 0: SQRT1_2 * f_0); entry N/2 - 1 + q holds f_{w/2} unscaled
+// SQRT1_2 * f_{k(a)} (a = 0: SQRT1_2 * f_0); entry N/2 - 1 + q holds SQRT1_2 * f_{w/2}
 // (the block-start pair, kernels.hip bfly_special / bfly_mixed).
 void twiddles(int n, std::vector<double>& tw) {
   const int L = n / 2;
@@ -144,10 +144,10 @@ void twiddles(int n, std::vector<double>& tw) {
       tw[2 * (off + a)] = kJsSqrt1_2 * fr[k];
       tw[2 * (off + a) + 1] = kJsSqrt1_2 * fi[k];
     }
-    // f_{w/2} unscaled (block-start pair) after the stage entries
+    // SQRT1_2 * f_{w/2} (block-start pair) after the stage entries
     const size_t fq = (size_t)(L - 1) + (size_t)(__builtin_ctz((unsigned)w) - 1);
-    tw[2 * fq] = fr[w / 2];
-    tw[2 * fq + 1] = fi[w / 2];
+    tw[2 * fq] = kJsSqrt1_2 * fr[w / 2];
+    tw[2 * fq + 1] = kJsSqrt1_2 * fi[w / 2];
     off += h;
   }
 }
