@@ -152,6 +152,42 @@ void twiddles(int n, std::vector<double>& tw) {
   }
 }
 
+// Coefficients of the mixed butterflies (kernels.hip bfly_mixed_tame), same indexing as
+// twiddles(): entry a > 0 of stage q holds (f_x, SQRT1_2 f_y) with f = f_{k(a)} unscaled;
+// entry 0 (the block-start pair) holds (1, 0), so that fma(b, R, L) is exactly jsfft's
+// left + right there; entry N/2 - 1 + q holds (f_{w/2,x}, SQRT1_2 f_{w/2,y}) (lane-uniform).
+void mixed_coeffs(int n, std::vector<double>& tm) {
+  const int L = n / 2;
+  int stages = 0;
+  for (int w = 2; w <= L; w <<= 1) ++stages;
+  tm.assign(2 * (size_t)(L - 1 + stages), 0.0);
+  size_t off = 0;
+  for (int w = 2; w <= L; w <<= 1) {
+    const int h = w / 2;
+    const double dr = cos(kJsPi / w), di = sin(kJsPi / w);
+    std::vector<double> fr(w), fi(w);
+    double r = 1, i = 0;
+    for (int j = 0; j < w; j++) {
+      fr[j] = r;
+      fi[j] = i;
+      const double t = r * dr - i * di;
+      i = r * di + i * dr;
+      r = t;
+    }
+    std::vector<int> kl;
+    klist(w, kl);
+    tm[2 * off] = 1.0;
+    for (int a = 1; a < h; a++) {
+      tm[2 * (off + a)] = fr[kl[a]];
+      tm[2 * (off + a) + 1] = kJsSqrt1_2 * fi[kl[a]];
+    }
+    const size_t fq = (size_t)(L - 1) + (size_t)(__builtin_ctz((unsigned)w) - 1);
+    tm[2 * fq] = fr[w / 2];
+    tm[2 * fq + 1] = kJsSqrt1_2 * fi[w / 2];
+    off += h;
+  }
+}
+
 // Mel filterbank as per-bin segment tables (kernels.hip mel_energies): bin k lies in
 // segment m with b_m <= k < b_{m+1}, m in [0, nf]; band j rises over segment j and falls
 // over segment j + 1 (mfcc.js:43-50). Bins at or past b_{nf+1} belong to no band.
@@ -309,6 +345,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   dct_table(nf, nc, dct.data());
   std::vector<double> tw;
   twiddles(n, tw);
+  std::vector<double> twm;
+  mixed_coeffs(n, twm);
   std::vector<float> twf(tw.size());
   for (size_t i = 0; i < tw.size(); ++i) twf[i] = (float)tw[i];
   std::vector<int> kl;
@@ -334,7 +372,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
-               o_twf = carve<float>(off, twf.size()), o_kl = carve<int>(off, L),
+               o_twf = carve<float>(off, twf.size()), o_twm = carve<double>(off, twm.size()),
+               o_kl = carve<int>(off, L),
                o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<float>(off, mwud.size()),
                o_seg = carve<uint8_t>(off, mseg.size()), o_dct = carve<float>(off, dct.size()),
                o_mb = carve<int32_t>(off, bins.size());
@@ -343,6 +382,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   put(o_win, d->window == MGX_WINDOW_HAMMING ? ham.data() : han.data(), n * sizeof(float));
   put(o_tw, tw.data(), tw.size() * sizeof(double));
   put(o_twf, twf.data(), twf.size() * sizeof(float));
+  put(o_twm, twm.data(), twm.size() * sizeof(double));
   put(o_kl, kl.data(), L * sizeof(int));
   put(o_lim, lim, sizeof lim);
   put(o_mw, mwud.data(), mwud.size() * sizeof(float));
@@ -357,6 +397,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->t.window = reinterpret_cast<const float*>(b + o_win);
   p->t.tw = reinterpret_cast<const double2*>(b + o_tw);
   p->t.twf = reinterpret_cast<const float2*>(b + o_twf);
+  p->t.twm = reinterpret_cast<const double2*>(b + o_twm);
   p->t.klist = reinterpret_cast<const int*>(b + o_kl);
   p->t.bblim = reinterpret_cast<const int*>(b + o_lim);
   p->t.mel_wud = reinterpret_cast<const float2*>(b + o_mw);

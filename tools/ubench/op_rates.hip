@@ -101,6 +101,23 @@ __global__ void k_cvt_rt(double* out, double a, double b) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// v_cndmask_b32_e64 with the lane mask in an SGPR pair from a ballot (the kernel's form)
+__global__ void k_cnd64(double* out, float a, float b) {
+  float x[8];
+  for (int c = 0; c < 8; ++c) x[c] = threadIdx.x * 1e-3f + c;
+  const unsigned long long m = __ballot(threadIdx.x & 1);
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(x[c]) : "v"(a), "s"(m));
+    }
+  }
+  float s = b;
+  for (int c = 0; c < 8; ++c) s += x[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 // Mixed streams: an f64 FMA followed by an f32 FMA on independent chains (can f32 work
 // fill f64 issue gaps?)
 __global__ void k_mix(double* out, double a, double b) {
@@ -160,7 +177,8 @@ int main() {
       {"mix f64 fma + f32 fma (2 instr)", k_mix, nullptr, 2},
       {"v_fma_f32", nullptr, k_fma32, 1},   {"v_add_f32", nullptr, k_add32, 1},
       {"v_rsq_f32", nullptr, k_rsq32, 1},   {"v_log_f32", nullptr, k_log32, 1},
-      {"v_cndmask_b32", nullptr, k_cnd, 1}, {"v_mov_b32_dpp", nullptr, k_dpp, 1},
+      {"v_cndmask_b32 (vcc)", nullptr, k_cnd, 1}, {"v_cndmask_b32_e64 (sgpr mask)", nullptr, k_cnd64, 1},
+      {"v_mov_b32_dpp", nullptr, k_dpp, 1},
       {"v_pk_fma_f32", nullptr, k_pkfma, 1}, {"v_pk_mul_f32", nullptr, k_pkmul, 1},
   };
   for (int rep = 0; rep < 2; ++rep) {
