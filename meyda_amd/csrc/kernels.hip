@@ -569,100 +569,90 @@ __device__ __forceinline__ int dpp_i(int v) {
   return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, true);
 }
 
-// One Hillis-Steele step of a segmented inclusive scan over lanes:
-// (f, u, d) <- (f_src | f, f ? (u, d) : (u_src + u, d_src + d)).
-template <int CTRL, int ROW_MASK = 0xF>
-__device__ __forceinline__ void seg_scan_step(int& f, float& u, float& d) {
-  const float nu = dpp_f<CTRL, ROW_MASK>(u), nd = dpp_f<CTRL, ROW_MASK>(d);
-  const int nf = dpp_i<CTRL, ROW_MASK>(f);
-  if (!f) {
-    u += nu;
-    d += nd;
+// Mel band energies of one frame, mfcc.js:40-62: E_j = sum_k w_jk p_k, p_k = a_k^2 (float32).
+// The triangular filters split the bins into segments m = [b_m, b_{m+1}): every bin
+// belongs to one segment, and band j = (rising half on segment j) + (falling half on
+// segment j+1). So E_j = U_j + D_{j+1} with U_m = sum_{k in m} up(k) p_k and
+// D_m = sum_{k in m} dn(k) p_k: two segmented sums over the bins, computed as in-lane
+// runs plus one segmented scan across the lanes. Where the segments start
+// does not depend on the frame, so every branch of that logic is a plan table
+// (plan.cpp mel_lane_tables): per bin a keep factor (0 restarts the sums) and the scratch
+// slot the running sums are stored to, per lane the keeps of the six scan steps and the two
+// slots of the head and tail totals. No selects, one packed multiply and one packed FMA per
+// bin, one DPP-fused FMA per scan step and sum. No cross-segment sums are formed, so there
+// is no cancellation; the sums are float32 like the reference's Float32Array accumulation,
+// in a different order.
+// The lane's record of the frame-independent mel tables (plan.cpp mel_lane_tables), issued
+// before the moment sums so that the load latency hides behind the reductions.
+template <int N>
+struct MelTab {
+  static constexpr int R = Geo<N>::R, W = mel_rec_words(R), B = (R + 3) / 4;
+  uint32_t w[W];
+  __device__ __forceinline__ void load(KArgs* ap, int lane) {
+    const auto src = gbl(ap->t.mel_rec) + W * lane;
+#pragma unroll
+    for (int i = 0; i < W; ++i) w[i] = src[i];
   }
-  f |= nf;
-}
+  __device__ __forceinline__ float rise(int jj) const { return __builtin_bit_cast(float, w[jj]); }
+  __device__ __forceinline__ uint32_t slot(int jj) const { return (w[R + jj / 4] >> (8 * (jj % 4))) & 0xFFu; }
+  __device__ __forceinline__ float keep(int jj) const { return (float)((w[R + B + jj / 4] >> (8 * (jj % 4))) & 0xFFu); }
+  __device__ __forceinline__ float scan_keep(int s) const { return (float)((w[R + 2 * B + s / 4] >> (8 * (s % 4))) & 0xFFu); }
+  __device__ __forceinline__ uint32_t head_slot() const { return (w[R + 2 * B + 1] >> 16) & 0xFFu; }
+  __device__ __forceinline__ uint32_t tail_slot() const { return w[R + 2 * B + 1] >> 24; }
+};
 
 // Mel band energies of one frame, mfcc.js:40-62: E_j = sum_k w_jk p_k, p_k = a_k^2 (float32).
 // The triangular filters split the bins into segments m = [b_m, b_{m+1}): every bin
 // belongs to one segment, and band j = (rising half on segment j) + (falling half on
 // segment j+1). So E_j = U_j + D_{j+1} with U_m = sum_{k in m} up(k) p_k and
 // D_m = sum_{k in m} dn(k) p_k: two segmented sums over the bins, computed as in-lane
-// runs plus one segmented scan across the lanes. No cross-segment sums
-// are ever formed, so there is no cancellation; the sums are float32 like the reference's
-// Float32Array accumulation, in a different order.
+// runs plus one segmented scan across the lanes. Where the segments start
+// does not depend on the frame, so every branch of that logic is a plan table (MelTab):
+// per bin a keep factor (0 restarts the sums) and the scratch slot the running sums are
+// stored to, per lane the keeps of the six scan steps and the slots of the head and tail
+// totals. No selects: per bin a packed multiply and a packed FMA, per scan step two DPP
+// moves and a packed FMA. No cross-segment sums are formed, so there is no cancellation;
+// the sums are float32 like the reference's Float32Array accumulation, in a different order
+// (and the falling weight is 1 - rising in float32, within an ulp of the f64 ratio).
 template <int N>
 __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>::R], int lane, float2* buf,
-                                             FrameRec& rec) {
+                                             FrameRec& rec, const MelTab<N>& mt) {
   constexpr int R = Geo<N>::R;
   const int nf = ap->nfilt;
-  float* mu = reinterpret_cast<float*>(buf);  // U[0..nf+1], slot nf+1 collects bins of no band
-  float* md = mu + (kMaxMel + 2 + 64);
+  float2* mud = buf;  // (U, D) of segments 0..nf+1, then the 64 head partials (kMelHead)
   wave_sync();  // band-sum reads of the prefix buffer are done
-  for (int i = lane; i < nf + 2; i += 64) {
-    mu[i] = 0.0f;
-    md[i] = 0.0f;
-  }
+  float2* mine = mud + lane;  // segment slot `lane` (and lane + 64), head slot kMelHead + lane
+  if (lane < nf + 2) mine[0] = make_float2(0.0f, 0.0f);
+  if (lane + 64 < nf + 2) mine[64] = make_float2(0.0f, 0.0f);
   wave_sync();
-  const auto wt = gbl(reinterpret_cast<const float*>(ap->t.mel_wud)) + 2 * R * lane;
-  // segment ids are bytes, R per lane, read as R/4 dwords (one 16-bit word when R = 2)
-  constexpr int SW = R >= 4 ? R / 4 : 1;
-  uint32_t sgw[SW];
-  if constexpr (R >= 4) {
-    const auto sg = gbl(reinterpret_cast<const uint32_t*>(ap->t.mel_seg)) + SW * lane;
-#pragma unroll
-    for (int i = 0; i < SW; ++i) sgw[i] = sg[i];
-  } else {
-    sgw[0] = gbl(reinterpret_cast<const uint16_t*>(ap->t.mel_seg))[lane];
-  }
-  float2 w[R];
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj) w[jj] = make_float2(wt[2 * jj], wt[2 * jj + 1]);  // (rising, falling) weight
-  auto seg_of = [&](int jj) { return (int)((sgw[jj >> 2] >> (8 * (jj & 3))) & 0xFFu); };
-  int prev = dpp_i<0x138>(seg_of(R - 1));  // wave_shr:1 -> segment of the previous lane's last bin
-  if (lane == 0) prev = nf + 1;
-  const int dummy = kMaxMel + 2 + lane;  // per-lane sink for the stores a bin does not make
-  float cu = 0.0f, cd = 0.0f, hu = 0.0f, hd = 0.0f;
-  int hseg = nf + 1, seen = 0;
+  f32x2 acc = {0.0f, 0.0f};
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) {
-    const int m = seg_of(jj);
     const float p = av[jj] * av[jj];  // powerSpectrum.js
-    // A bin that starts a segment closes the open one (it ended at the previous bin): an
-    // interior segment is stored now, the lane's first one waits for the carry (head).
-    const bool b = m != prev;
-    const bool st = b && seen, hd_now = b && !seen;
-    const int at = st ? prev : dummy;
-    mu[at] = cu;
-    md[at] = cd;
-    hu = hd_now ? cu : hu;
-    hd = hd_now ? cd : hd;
-    hseg = hd_now ? prev : hseg;
-    seen |= b;
-    cu = __builtin_fmaf(w[jj].x, p, b ? 0.0f : cu);
-    cd = __builtin_fmaf(w[jj].y, p, b ? 0.0f : cd);
-    prev = m;
+    mud[mt.slot(jj)] = make_float2(acc.x, acc.y);
+    const float up = mt.rise(jj), kp = mt.keep(jj);
+    const f32x2 w = {up, 1.0f - up}, pp = {p, p}, kk = {kp, kp};
+    acc = __builtin_elementwise_fma(w, pp, acc * kk);
   }
-  // segmented inclusive scan of (seen, tail sums) over the lanes
-  int f = seen;
-  float su = cu, sd = cd;
-  seg_scan_step<0x111>(f, su, sd);  // row_shr:1
-  seg_scan_step<0x112>(f, su, sd);  // row_shr:2
-  seg_scan_step<0x114>(f, su, sd);  // row_shr:4
-  seg_scan_step<0x118>(f, su, sd);  // row_shr:8
-  seg_scan_step<0x142, 0xA>(f, su, sd);  // row_bcast:15
-  seg_scan_step<0x143, 0xC>(f, su, sd);  // row_bcast:31
-  const float xu = dpp_f<0x138>(su), xd = dpp_f<0x138>(sd);  // exclusive: carry into this lane
-  if (seen) {
-    mu[hseg] = xu + hu;
-    md[hseg] = xd + hd;
-  }
-  if (lane == 63) {  // the segment still open at the last bin
-    mu[prev] = su;
-    md[prev] = sd;
-  }
+  // segmented inclusive scan of the lane tails: s += keep_s * s_src (keep_s = 0 once the
+  // lanes summed so far hold a segment start; a missing source lane reads 0)
+  f32x2 sc = acc;
+  auto step = [&](float u, float d, int s) {
+    const f32x2 src = {u, d}, ks = {mt.scan_keep(s), mt.scan_keep(s)};
+    sc = __builtin_elementwise_fma(src, ks, sc);
+  };
+  step(dpp_f<0x111>(sc.x), dpp_f<0x111>(sc.y), 0);  // row_shr:1
+  step(dpp_f<0x112>(sc.x), dpp_f<0x112>(sc.y), 1);  // row_shr:2
+  step(dpp_f<0x114>(sc.x), dpp_f<0x114>(sc.y), 2);  // row_shr:4
+  step(dpp_f<0x118>(sc.x), dpp_f<0x118>(sc.y), 3);  // row_shr:8
+  step(dpp_f<0x142, 0xA>(sc.x), dpp_f<0x142, 0xA>(sc.y), 4);  // row_bcast:15 (rows 1, 3)
+  step(dpp_f<0x143, 0xC>(sc.x), dpp_f<0x143, 0xC>(sc.y), 5);  // row_bcast:31 (rows 2, 3)
+  const float xu = dpp_f<0x138>(sc.x), xd = dpp_f<0x138>(sc.y);  // exclusive: carry into this lane (wave_shr:1)
+  const float2 hp = mine[kMelHead];
+  mud[mt.head_slot()] = make_float2(xu + hp.x, xd + hp.y);  // the segment this lane's first start closes
+  mud[mt.tail_slot()] = make_float2(sc.x, sc.y);           // lane 63: the segment still open at the last bin
   wave_sync();
-  if (lane < nf) rec.lm[lane] = mu[lane] + md[lane + 1];
-  if (lane + 64 < nf) rec.lm[lane + 64] = mu[lane + 64] + md[lane + 65];
+  if (lane < nf) rec.lm[lane] = mine[0].x + mine[1].y;  // nf <= kMaxMel = 64
 }
 
 // Bark-band sums and mel energies of a frame with a non-finite amplitude, summed exactly
@@ -889,6 +879,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
 
 #ifndef MGX_ABL_NO_REDUCE
+  MelTab<N> mt;
+  if (ap->need_mfcc) mt.load(ap, lane);
   // Per-frame reductions, lane t owns bins [R t, R t + R).
   float av[R];
 #pragma unroll
@@ -982,7 +974,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   if (!(total < __builtin_huge_val())) {
     nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
   } else if (ABL_ON(MELSCAN) && ap->need_mfcc) {
-    mel_energies<N>(ap, av, lane, buf, rec);
+    mel_energies<N>(ap, av, lane, buf, rec, mt);
   }
   if constexpr (kMomLds) {
     wave_sync();

@@ -11,6 +11,10 @@ constexpr int kMaxMel = 64;
 constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
+constexpr int kMelHead = kMaxMel + 2;  // mel scratch: segment sums [0, nfilt + 2), head partials from here
+// dwords of one lane's mel record for R bins per lane (R weights, R slot bytes, R keep bytes,
+// 8 bytes of scan keeps and slots), padded to whole 16-byte loads
+__host__ __device__ constexpr int mel_rec_words(int R) { return (R + 2 * ((R + 3) / 4) + 2 + 3) / 4 * 4; }
 // Device-resident, read-only tables of a plan (one allocation, see plan.cpp).
 struct DevTables {
   const float* window;       // N, the selected window (src/meyda.js:116-138)
@@ -19,8 +23,7 @@ struct DevTables {
   const double2* twm;        // like tw: (b, c0) per slot pair of the mixed butterflies (plan.cpp mixed_coeffs)
   const int* klist;          // N/2: slot location -> spectrum bin
   const int* bblim;          // 25 bark band limits (loudness.js:24-45)
-  const float2* mel_wud;     // N/2: (rising, falling) filter weight of each bin in its segment (mfcc.js:40-51)
-  const uint8_t* mel_seg;    // N/2: segment m of each bin (b_m <= k < b_{m+1}); nfilt + 1 = no band
+  const uint32_t* mel_rec;   // 64 per-lane records of the mel segment tables (plan.cpp mel_lane_tables)
   const int* mel_bins;       // nfilt + 2 filter edges (mfcc.js:15-38), for the non-finite-frame path
   const float* dct;          // ncoef * nfilt, dct[c + j*ncoef] (mfcc.js:67-83)
 };

@@ -205,6 +205,67 @@ void mel_segments(const int32_t* b, int nf, int L, std::vector<float>& wud, std:
   }
 }
 
+// Per-lane form of the segment tables for kernels.hip mel_energies (lane t owns bins
+// [R t, R t + R), R = L / 64), one record of mgx::mel_rec_words(R) dwords per lane:
+//   R floats      rising weight of each bin (the falling one is 1 - rising in the kernel)
+//   R bytes       the scratch slot the running sums are stored to before the bin is added
+//   R bytes       keep (1, or 0 where a segment starts: the sums restart)
+//   8 bytes       keeps (0/1) of the 6 segmented-scan steps, head-total slot, tail slot
+// Slots index float2 (U, D) entries of the wave's mel scratch: 0..nf+1 the segments (nf+1
+// collects the bins of no band, and bin -1), kMelHead + t the head partial of lane t. Up
+// to and including the lane's first segment start the sums go to the lane's head slot (the
+// last of these stores is the lane's partial of the segment that began in an earlier lane,
+// completed with the carry of the segmented scan), afterwards to that segment's slot (final
+// at the start that closes it, a running partial that a later store overwrites otherwise;
+// only this lane stores there in the loop, so lanes inside one long segment never store to
+// one address together). The scan keeps replay the flag logic of a Hillis-Steele segmented
+// scan over the kernel's DPP steps (row_shr 1, 2, 4, 8; row_bcast 15 on rows 1, 3;
+// row_bcast 31 on rows 2, 3), which depends only on which lanes hold a segment start.
+void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& wud, int nf, int L,
+                     std::vector<uint32_t>& rec) {
+  const int R = L / 64, sink = nf + 1, W = mgx::mel_rec_words(R);
+  rec.assign((size_t)W * 64, 0u);
+  bool seen[64];
+  for (int t = 0; t < 64; ++t) {
+    uint32_t* r = &rec[(size_t)W * t];
+    uint8_t* slots = reinterpret_cast<uint8_t*>(r + R);
+    uint8_t* keeps = slots + 4 * ((R + 3) / 4);
+    uint8_t* lane8 = keeps + 4 * ((R + 3) / 4);
+    seen[t] = false;
+    int hseg = sink;
+    for (int jj = 0; jj < R; ++jj) {
+      const int k = R * t + jj;
+      const int prevseg = k == 0 ? sink : seg[k - 1];
+      const bool start = seg[k] != prevseg;
+      slots[jj] = (uint8_t)(seen[t] ? prevseg : mgx::kMelHead + t);
+      if (start && !seen[t]) {
+        seen[t] = true;
+        hseg = prevseg;
+      }
+      keeps[jj] = start ? 0 : 1;
+      memcpy(&r[jj], &wud[2 * k], 4);
+    }
+    lane8[6] = (uint8_t)(seen[t] ? hseg : mgx::kMelHead + t);
+    lane8[7] = (uint8_t)(t == 63 ? seg[L - 1] : mgx::kMelHead + t);
+  }
+  bool f[64];
+  for (int t = 0; t < 64; ++t) f[t] = seen[t];
+  for (int s = 0; s < 6; ++s) {
+    bool g[64];
+    for (int t = 0; t < 64; ++t) {
+      const int row = t / 16;
+      int src = -1;
+      if (s < 4) src = (t % 16) >= (1 << s) ? t - (1 << s) : -1;
+      else if (s == 4) src = (row == 1 || row == 3) ? row * 16 - 1 : -1;
+      else src = (row == 2 || row == 3) ? 31 : -1;
+      uint8_t* lane8 = reinterpret_cast<uint8_t*>(&rec[(size_t)W * t + R]) + 8 * ((R + 3) / 4);
+      lane8[s] = f[t] ? 0 : 1;
+      g[t] = f[t] || (src >= 0 && f[src]);
+    }
+    memcpy(f, g, sizeof f);
+  }
+}
+
 int validate(const mgx_plan_desc* d) {
   if (!d) return fail(MGX_E_INVALID_ARGUMENT, "plan descriptor is NULL");
   if (d->struct_size != sizeof(mgx_plan_desc))
@@ -354,6 +415,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   std::vector<float> mwud;
   std::vector<uint8_t> mseg;
   mel_segments(bins.data(), nf, L, mwud, mseg);
+  std::vector<uint32_t> mrec;
+  mel_lane_tables(mseg, mwud, nf, L, mrec);
 
   auto* p = new mgx_plan();
   p->d = *d;
@@ -374,8 +437,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
                o_twf = carve<float>(off, twf.size()), o_twm = carve<double>(off, twm.size()),
                o_kl = carve<int>(off, L),
-               o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<float>(off, mwud.size()),
-               o_seg = carve<uint8_t>(off, mseg.size()), o_dct = carve<float>(off, dct.size()),
+               o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<uint32_t>(off, mrec.size()), o_dct = carve<float>(off, dct.size()),
                o_mb = carve<int32_t>(off, bins.size());
   std::vector<unsigned char> host(off, 0);
   auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) memcpy(host.data() + at, src, bytes); };
@@ -385,8 +447,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   put(o_twm, twm.data(), twm.size() * sizeof(double));
   put(o_kl, kl.data(), L * sizeof(int));
   put(o_lim, lim, sizeof lim);
-  put(o_mw, mwud.data(), mwud.size() * sizeof(float));
-  put(o_seg, mseg.data(), mseg.size());
+  put(o_mw, mrec.data(), mrec.size() * sizeof(uint32_t));
   put(o_mb, bins.data(), bins.size() * sizeof(int32_t));
   put(o_dct, dct.data(), dct.size() * sizeof(float));
   e = hipMalloc(reinterpret_cast<void**>(&p->dev), off);
@@ -400,8 +461,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->t.twm = reinterpret_cast<const double2*>(b + o_twm);
   p->t.klist = reinterpret_cast<const int*>(b + o_kl);
   p->t.bblim = reinterpret_cast<const int*>(b + o_lim);
-  p->t.mel_wud = reinterpret_cast<const float2*>(b + o_mw);
-  p->t.mel_seg = reinterpret_cast<const uint8_t*>(b + o_seg);
+  p->t.mel_rec = reinterpret_cast<const uint32_t*>(b + o_mw);
   p->t.mel_bins = reinterpret_cast<const int*>(b + o_mb);
   p->t.dct = reinterpret_cast<const float*>(b + o_dct);
   *out = p;
