@@ -93,11 +93,16 @@ struct Geo {
 #endif
   static constexpr int FB = 4 * FPW;        // frames per workgroup iteration
   // Register budget (VGPRs + AGPRs): 4 waves/SIMD (<= 128) up to N = 1024, where LDS
-  // allows 4 workgroups per CU; 2 waves (<= 256) at N = 2048. Without the bound the
-  // allocator drifts past the threshold (129 VGPRs, or 251 + 32 AGPRs) and occupancy halves.
+  // allows 4 workgroups per CU; 3 waves (<= 168) at N = 2048 (without the frame prefetch:
+  // measured 3 % faster than 2 waves with it). Without the bound the allocator drifts past
+  // the threshold (129 VGPRs, or 251 + 32 AGPRs) and occupancy drops.
   // N = 256 fits 6 waves (<= 80 VGPRs; measured 2.5 % faster than 5); at N = 512 a bound
   // of 5 waves measured slower than 4.
-  static constexpr int WPE = N <= 256 ? 6 : N <= 1024 ? 4 : 2;
+#ifdef MGX_WPE2048
+  static constexpr int WPE = N <= 256 ? 6 : N <= 1024 ? 4 : MGX_WPE2048;
+#else
+  static constexpr int WPE = N <= 256 ? 6 : N <= 1024 ? 4 : 3;
+#endif
   // Slot buffer entries (8 bytes): the padded exchange image, the natural-order half
   // spectrum X[0..L] (complex output), the padded prefix row (pd) and the mel scratch.
   static constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -112,6 +117,15 @@ struct Geo {
   static constexpr bool MOM_LDS = N <= 1024;
 #endif
   static constexpr int MOM_STRIDE = 72;
+  // Register prefetch of the next frame. A vector-memory wait is in issue order (vmcnt),
+  // so the first table load a frame waits on (window, twiddles) also waits for the
+  // prefetch issued before it: at N = 1024 loading each frame when its wave starts it
+  // measured 2.7 % faster (and frees 16 VGPRs); at N = 512 and 2048 the prefetch wins.
+#ifdef MGX_PREFETCH_ALL
+  static constexpr bool PREFETCH = MGX_PREFETCH_ALL;
+#else
+  static constexpr bool PREFETCH = N <= 512;
+#endif
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
 
@@ -1113,9 +1127,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   const uint64_t g0 = (uint64_t)blockIdx.x * per, g1 = g0 + per < ng ? g0 + per : ng;
   const uint64_t b0 = g0 * 4 + wave, bend = g1 * 4 < nb ? g1 * 4 : nb;
 #endif
-  // Register prefetch: the next frame of this wave is loaded while this one is processed.
   // Loads are unconditional (the frame index is clamped; results of frames past the end
   // are never stored), so they issue back to back with no branches or waits between them.
+  // With G::PREFETCH the next frame of the wave is loaded while this one is processed.
   auto load = [&](float (&xv)[CH], uint64_t b, int j) {
     uint64_t f = b * FPW + j;
     f = f < nf ? f : nf - 1;
@@ -1123,8 +1137,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
 #pragma unroll
     for (int c = 0; c < CH; ++c) xv[c] = xin[c * 64 + lane];
   };
-  float xn[CH];
-  load(xn, b0, 0);
+
+  float xn[G::PREFETCH ? CH : 1];
+  if constexpr (G::PREFETCH) load(xn, b0, 0);
 
   for (uint64_t b = b0; b < bend; b += wstride) {
     const uint64_t f0 = b * FPW;
@@ -1132,10 +1147,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     for (int j = 0; j < FPW; ++j) {
       const uint64_t f = f0 + j;
       float x[CH];
+      if constexpr (G::PREFETCH) {
 #pragma unroll
-      for (int c = 0; c < CH; ++c) x[c] = xn[c];
-      if (j + 1 < FPW) load(xn, b, j + 1);
-      else load(xn, b + wstride, 0);
+        for (int c = 0; c < CH; ++c) x[c] = xn[c];
+        if (j + 1 < FPW) load(xn, b, j + 1);
+        else load(xn, b + wstride, 0);
+      } else {
+        load(x, b, j);
+      }
       frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs);
     }
     wave_sync();
