@@ -98,10 +98,13 @@ struct Geo {
   // the threshold (129 VGPRs, or 251 + 32 AGPRs) and occupancy drops.
   // N = 256 fits 6 waves (<= 80 VGPRs; measured 2.5 % faster than 5); at N = 512 a bound
   // of 5 waves measured slower than 4.
+#ifndef MGX_WPE1024
+#define MGX_WPE1024 4
+#endif
 #ifdef MGX_WPE2048
-  static constexpr int WPE = N <= 256 ? 6 : N <= 1024 ? 4 : MGX_WPE2048;
+  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? 4 : N <= 1024 ? MGX_WPE1024 : MGX_WPE2048;
 #else
-  static constexpr int WPE = N <= 256 ? 6 : N <= 1024 ? 4 : 3;
+  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? 4 : N <= 1024 ? MGX_WPE1024 : 3;
 #endif
   // Slot buffer entries (8 bytes): the padded exchange image, the natural-order half
   // spectrum X[0..L] (complex output), the padded prefix row (pd) and the mel scratch.
@@ -568,8 +571,14 @@ struct Lds {
   static constexpr size_t mom_bytes = G::MOM_LDS ? (size_t)4 * 5 * G::MOM_STRIDE * 8 : 0;
   // Frame records: FPW per wave.
   static constexpr size_t rec_off = mom_off + mom_bytes;
+  // Kernel constants read per lane, staged once per workgroup: the 13 scalar output
+  // pointers and the 25 bark band limits. Read from LDS (lgkmcnt) rather than global
+  // memory: a vector-memory wait is in issue order (vmcnt), so a global read here would
+  // also wait for every output store and frame load issued before it.
+  static constexpr size_t kc_off = rec_off + (size_t)G::FB * sizeof(FrameRec);
+  static constexpr size_t kc_bytes = 16 * 8 + 32 * 4;
   // The DCT table (mfcc.js:67-83), staged once per workgroup, sized per plan.
-  static constexpr size_t dct_off = rec_off + (size_t)G::FB * sizeof(FrameRec);
+  static constexpr size_t dct_off = kc_off + kc_bytes;
   static size_t bytes(int ncoef, int nfilt) { return dct_off + (size_t)ncoef * ((nfilt + 7) & ~7) * 4; }
 };
 
@@ -708,7 +717,8 @@ __device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av
 template <int N, bool FAITH, bool LITERAL>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
                                              int lane, const int (&lp)[Geo<N>::NPASS], const int (&kl)[Geo<N>::R],
-                                             bool dc_lane, float2* buf, double* mom, FrameRec* recs) {
+                                             bool dc_lane, float2* buf, double* mom, FrameRec* recs,
+                                             const int* klim) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
@@ -972,8 +982,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
   }
   if (lane < kBark) {
-    const auto lim = gbl(ap->t.bblim);
-    rec.band[lane] = pbuf[pd(lim[lane + 1])] - pbuf[pd(lim[lane])];
+    rec.band[lane] = pbuf[pd(klim[lane + 1])] - pbuf[pd(klim[lane])];  // limits staged in LDS
   }
   if (lane == 0) {
     rec.S[0] = total;
@@ -1091,7 +1100,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off) + wave * FPW;  // this wave's records
   KArgs* ap = args_ptr();
 
-  // The DCT table, once per workgroup (the only workgroup barrier of the kernel).
+  // Kernel constants and the DCT table, once per workgroup (the only workgroup barrier).
+  {
+    void** kptr = reinterpret_cast<void**>(smem + LY::kc_off);
+    int* klim = reinterpret_cast<int*>(smem + LY::kc_off + 16 * 8);
+    if (threadIdx.x < MGX_NUM_SCALARS) kptr[threadIdx.x] = ap->out.scalars[threadIdx.x];
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = gbl(ap->t.bblim)[threadIdx.x - 64];
+  }
   if (ap->need_spectrum && ap->need_mfcc) {
     const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
     const auto dct = gbl(ap->t.dct);
@@ -1155,7 +1170,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       } else {
         load(x, b, j);
       }
-      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs);
+      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
+                                      reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8));
     }
     wave_sync();
 
@@ -1271,7 +1287,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       for (int i = l2; ABL_ON(FIN) && i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {
         const int sc = i / FPW, fb = i % FPW;
         const uint64_t f = f0 + fb;
-        void* dst = q->out.scalars[sc];
+        void* dst = reinterpret_cast<void* const*>(smem + LY::kc_off)[sc];
         if (f >= q->num_frames || dst == nullptr) continue;
         const double v = scalar_value<N>(q, recs[fb], sc);
         if (q->scalar_f64) gbl(static_cast<double*>(dst))[f] = v;
