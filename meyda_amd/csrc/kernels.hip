@@ -121,14 +121,20 @@ struct Geo {
 #endif
   static constexpr int MOM_STRIDE = 72;
   // Register prefetch of the next frame. A vector-memory wait is in issue order (vmcnt),
-  // so the first table load a frame waits on (window, twiddles) also waits for the
-  // prefetch issued before it: at N = 1024 loading each frame when its wave starts it
-  // measured 2.7 % faster (and frees 16 VGPRs); at N = 512 and 2048 the prefetch wins.
-#ifdef MGX_PREFETCH_ALL
-  static constexpr bool PREFETCH = MGX_PREFETCH_ALL;
+  // so a table load a frame waits on (window, twiddles) also waits for a prefetch issued
+  // before it: prefetching at the start of the frame made every frame wait for the next
+  // one's HBM read at its window step (at N = 1024 loading each frame only when its wave
+  // starts it was 2.7 % faster).
+// PF = 1 loads the next frame at the start of this one; PF = 2 issues it in the middle of
+  // this frame, after the last table loads this frame waits on (twiddles: the passes are
+  // done; the mel records: issued just before), so no wait of this frame is held up by
+  // it; PF = 0 loads each frame when its wave starts it.
+#ifdef MGX_PF_ALL
+  static constexpr int PF = MGX_PF_ALL;
 #else
-  static constexpr bool PREFETCH = N <= 512;
+  static constexpr int PF = N <= 256 ? 1 : N <= 1024 ? 2 : 0;  // measured best per N
 #endif
+  static constexpr bool PREFETCH = PF != 0;
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
 
@@ -718,13 +724,23 @@ template <int N, bool FAITH, bool LITERAL>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
                                              int lane, const int (&lp)[Geo<N>::NPASS], const int (&kl)[Geo<N>::R],
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
-                                             const int* klim) {
+                                             const int* klim, float (&xn)[Geo<N>::PREFETCH ? Geo<N>::CH : 1],
+                                             GF next) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
   float* amp = reinterpret_cast<float*>(buf);  // the frame's amplitude row, once the FFT is done
   double* pbuf = reinterpret_cast<double*>(buf);
 
+  // mid-frame prefetch of the next frame (G::PF == 2), after the mel records are issued
+  // (frames without spectral features: right away)
+  auto prefetch_next = [&]() {
+    if constexpr (G::PF == 2) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) xn[c] = next[c * 64];
+    }
+  };
+  if (!ap->need_spectrum) prefetch_next();  // time-only features: no table loads follow
   // rms.js / energy.js: sum of squares; zcr.js: sign changes of adjacent samples,
   // `x >= 0` vs `x < 0` (so -0 is non-negative and NaN never counts).
   // Sum of squares as packed float32 FMAs over pairs of chunks; zcr from one ballot per
@@ -773,7 +789,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     recs[fb].energy = e;
     recs[fb].zcr = z;
   }
-  if (!ap->need_spectrum) return;
+  if (!ap->need_spectrum) return;  // (the prefetch was issued at the top: nothing to wait on)
   // Every sample finite and |x| <= 2^50 (each lane's sum of squares <= 2^100, not NaN):
   // no stage of the FFT can reach an infinity (bfly_mixed_tame).
 #if defined(MGX_ABL_NOTAME)
@@ -903,8 +919,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
 
 #ifndef MGX_ABL_NO_REDUCE
-  MelTab<N> mt;
-  if (ap->need_mfcc) mt.load(ap, lane);
   // Per-frame reductions, lane t owns bins [R t, R t + R).
   float av[R];
 #pragma unroll
@@ -967,6 +981,14 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     pk += (double)av[jj];
   }
   const int roll_m = (total > thr) ? cnt - 1 : L;
+  // The lane's mel records, then (G::PF == 2) the next frame: issued after the last table
+  // load this frame waits on before them, so no wait of this frame is held up by the
+  // prefetch; the band and mel sums, the moment finish and phase 2 run while it is in
+  // flight. (Issued any earlier, the extra live registers spill around the moment sums,
+  // and a spill reload is a vector-memory wait behind the prefetch.)
+  MelTab<N> mt;
+  if (ap->need_mfcc) mt.load(ap, lane);
+  prefetch_next();
   if constexpr (!kMomLds) {
 #ifdef MGX_ABL_NOWSUM
     const double S1 = readlane_d(P1, 63), S2 = readlane_d(P2, 63), S3 = readlane_d(P3, 63), S4 = readlane_d(P4, 63);
@@ -1145,12 +1167,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // Loads are unconditional (the frame index is clamped; results of frames past the end
   // are never stored), so they issue back to back with no branches or waits between them.
   // With G::PREFETCH the next frame of the wave is loaded while this one is processed.
-  auto load = [&](float (&xv)[CH], uint64_t b, int j) {
+  auto frame_ptr = [&](uint64_t b, int j) {
     uint64_t f = b * FPW + j;
     f = f < nf ? f : nf - 1;
-    const auto xin = gbl(args_ptr()->frames) + f * (uint64_t)N;
+    return (GF)(gbl(args_ptr()->frames) + f * (uint64_t)N + lane);
+  };
+  auto load = [&](float (&xv)[CH], uint64_t b, int j) {
+    const GF xin = frame_ptr(b, j);
 #pragma unroll
-    for (int c = 0; c < CH; ++c) xv[c] = xin[c * 64 + lane];
+    for (int c = 0; c < CH; ++c) xv[c] = xin[c * 64];
   };
 
   float xn[G::PREFETCH ? CH : 1];
@@ -1162,16 +1187,21 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     for (int j = 0; j < FPW; ++j) {
       const uint64_t f = f0 + j;
       float x[CH];
-      if constexpr (G::PREFETCH) {
+      GF next = nullptr;
+      if constexpr (G::PF == 1) {
 #pragma unroll
         for (int c = 0; c < CH; ++c) x[c] = xn[c];
         if (j + 1 < FPW) load(xn, b, j + 1);
         else load(xn, b + wstride, 0);
+      } else if constexpr (G::PF == 2) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) x[c] = xn[c];
+        next = frame_ptr(j + 1 < FPW ? b : b + wstride, j + 1 < FPW ? j + 1 : 0);
       } else {
         load(x, b, j);
       }
       frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
-                                      reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8));
+                                      reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next);
     }
     wave_sync();
 
