@@ -146,3 +146,49 @@ def test_randomized_plans(capi, oracle_mod):
         except AssertionError as e:
             raise AssertionError("case %d: n=%d window=%s sr=%g nmel=%d F=%d kind=%d: %s"
                                  % (case, n, window, sr, nmel, F, kind, e))
+
+
+SUBSETS = {
+    "time_only": ["rms", "energy", "zcr"],
+    "spectral": ["spectralCentroid", "spectralFlatness", "spectralKurtosis", "spectralRolloff"],
+    "loudness": ["loudness", "perceptualSharpness"],
+    "mfcc_only": ["mfcc"],
+    "amp_centroid": ["amplitudeSpectrum", "spectralCentroid"],
+}
+SCALAR_INDEX = {k: i for i, k in enumerate(SCALARS)}
+
+
+@pytest.mark.parametrize("n", [256, 512, 1024, 2048])
+def test_feature_subsets_across_batches(capi, oracle_mod, n):
+    """Each feature subset (the kernel skips the spectrum, the mel records or phase-2 parts
+    per request) over a batch spanning several frame batches per wave, so every frame is
+    fed by the next-frame load of the previous one (kernels.hip Geo::PF), mixing tame frames
+    with huge finite ones (|x| ~ 1e30: the two-form block-start butterflies) and silence
+    (the f64 amplitude path)."""
+    rng = np.random.default_rng(n)
+    F = 3001
+    x = rng.uniform(-1, 1, (F, n)).astype(np.float32)
+    x[5::7] *= np.float32(1e30)
+    x[3::11] = 0.0
+    ref = oracle_mod.extract(x)
+    plan = capi.Plan(buffer_size=n, scalar_f64=True)
+    for name, feats in SUBSETS.items():
+        out = plan.extract(x, feats)
+        for k in feats:
+            if k == "amplitudeSpectrum":
+                bad, _ = tolerance.check_spectra(out[k], ref["amp"])
+                assert not bad, (name, k, bad[:5])
+            elif k == "mfcc":
+                assert not tolerance.check_vectors(out[k], ref["mfcc"]), (name, k)
+            elif k == "loudness":
+                assert not tolerance.check_vectors(out["loudness.specific"], ref["loudness_specific"]), name
+                i = SCALAR_INDEX["loudness.total"]
+                got = np.asarray(out["loudness.total"], np.float64)[:, None]
+                assert not tolerance.check_scalars(got, ref["scalars"][:, i:i + 1], ref["amp"], n,
+                                                   names=["loudnessTotal"]), name
+            else:
+                i = SCALAR_INDEX[k]
+                got = np.asarray(out[k], np.float64)[:, None]
+                fails = tolerance.check_scalars(got, ref["scalars"][:, i:i + 1], ref["amp"], n,
+                                                names=[tolerance.SCALAR_NAMES[i]])
+                assert not fails, (name, k, fails[:5])
