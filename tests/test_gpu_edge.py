@@ -166,7 +166,9 @@ def test_feature_subsets_across_batches(capi, oracle_mod, n):
     with huge finite ones (|x| ~ 1e30: the two-form block-start butterflies) and silence
     (the f64 amplitude path)."""
     rng = np.random.default_rng(n)
-    F = 3001
+    # >= 2 groups of 16 frames per workgroup at every N (at most 6 x 256 workgroups), so
+    # waves run several batches and cross batch boundaries with the next-frame load
+    F = 1536 * 16 * 2 + 5
     x = rng.uniform(-1, 1, (F, n)).astype(np.float32)
     x[5::7] *= np.float32(1e30)
     x[3::11] = 0.0
