@@ -515,7 +515,9 @@ struct FrameRec {
 // f32 hardware log (m_hi = (float)m); y = 0.23 log2 x in double; 2^y = 2^floor(y) 2^frac(y)
 // with the f32 hardware exp2 on [0, 1). Relative error ~1e-7 (a float32 ulp or two).
 __device__ __forceinline__ float pow023(double x) {
-  if (!(x > 0.0 && x < __builtin_huge_val())) return (float)pow(x, 0.23);  // 0, inf, NaN
+  // 0, inf, NaN (a band sum is never negative): pow's values, without the library routine
+  // (its f64 log/exp code would run for a whole wave whenever one band of a frame is silent)
+  if (!(x > 0.0 && x < __builtin_huge_val())) return x == 0.0 ? 0.0f : x > 0.0 ? __builtin_huge_valf() : (float)x;
   int e;
   const double m = 2.0 * frexp(x, &e);  // [1, 2)
   const float mh = (float)m, ml = (float)(m - (double)mh);
@@ -529,7 +531,8 @@ __device__ __forceinline__ float pow023(double x) {
 // Math.log(x) of a float32, rounded to float32 (mfcc.js:64): ln x = (e + log2 m) ln 2 with
 // x = m 2^e, m in [1, 2) exact and log2 m from the f32 hardware log; |error| ~4e-8 absolute.
 __device__ __forceinline__ float ln_f32(float x) {
-  if (!(x > 0.0f && x < __builtin_huge_valf())) return (float)log((double)x);  // 0, inf, NaN, < 0
+  // 0 -> -inf, inf -> inf, NaN -> NaN (a mel energy is never negative), as Math.log
+  if (!(x > 0.0f && x < __builtin_huge_valf())) return x == 0.0f ? -__builtin_huge_valf() : x;
   int e;
   const float m = 2.0f * frexpf(x, &e);
   return (float)(((double)(e - 1) + (double)__builtin_amdgcn_logf(m)) * kLn2);
@@ -1055,10 +1058,11 @@ __device__ __forceinline__ double dct_sum(const float* dct, const float* lm, int
 }
 
 // 2^y in double for the geometric mean of spectralFlatness.js: 2^floor(y) * 2^frac(y) with
-// the f32 hardware exp2 on [0, 1) (relative error ~1.5e-7, against the 1e-5 bar); |y|
-// beyond the f32 exponent range (a zero amplitude makes y = -inf) takes the library exp2.
+// the f32 hardware exp2 on [0, 1) (relative error ~1.5e-7, against the 1e-5 bar).
 __device__ __forceinline__ double exp2_mean(double y) {
-  if (!(__builtin_fabs(y) < 1000.0)) return exp2(y);
+  // -inf (a zero amplitude) -> 0, +inf -> inf, NaN -> NaN; v_ldexp_f64 saturates to 0 / inf
+  // for any exponent the int conversion holds
+  if (!(__builtin_fabs(y) < 1e9)) return y != y ? y : y > 0.0 ? __builtin_huge_val() : 0.0;
   const double n = floor(y);
   return ldexp((double)__builtin_amdgcn_exp2f((float)(y - n)), (int)n);
 }
@@ -1240,8 +1244,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
           // rows 2r and 2r+1 hold one frame: row_bcast:15 adds row 2r's total into row 2r+1
           tot += dpp_d<0x142, 0xA>(tot); mx = fmaxf(mx, dpp_f<0x142, 0xA>(mx)); sh += dpp_f<0x142, 0xA>(sh);
           if (bnd == 31 && f < q->num_frames) {
-            const double ps = (tot - (double)mx) / tot;
-            const double sv[3] = {tot, ps * ps, ((double)sh + q->sharp_tail_sum) * (0.11 / tot)};
+            const double rt = 1.0 / tot;  // one division for both quotients (<= 1 ulp apart)
+            const double ps = (tot - (double)mx) * rt;
+            const double sv[3] = {tot, ps * ps, ((double)sh + q->sharp_tail_sum) * (0.11 * rt)};
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
               void* dst = q->out.scalars[MGX_LOUDNESS_TOTAL + k];
