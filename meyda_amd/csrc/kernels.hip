@@ -492,11 +492,14 @@ __device__ __forceinline__ float slot_amp_rsq(float re, float im, bool& ok) {
   const double xr = re, xi = im;
   const double s = __builtin_fma(xr, xr, xi * xi);
   const float sf = (float)s;
-  ok = sf >= 0x1p-120f && sf <= 0x1p120f;
   const float q = __builtin_amdgcn_rsqf(sf);
   const double y = (double)(sf * q);
   const double r = __builtin_fma(-y, y, s);
-  return (float)__builtin_fma(r, (double)(0.5f * q), y);
+  const float a = (float)__builtin_fma(r, (double)(0.5f * q), y);
+  // s in [2^-120, 2^120] <=> a in [2^-60, 2^60] (outside, the rsq seed is a denormal, 0,
+  // inf or NaN and so is a, or a is out of range): float32 compares instead of f64 ones
+  ok = a >= 0x1p-60f && a <= 0x1p60f;
+  return a;
 }
 
 struct FrameRec {
