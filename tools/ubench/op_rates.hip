@@ -140,6 +140,55 @@ __global__ void k_mix(double* out, double a, double b) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = x0 + x1 + x2 + x3 + y0 + y1 + y2 + y3;
 }
 
+
+// Matrix-core f64: issue cost of v_mfma_f64_16x16x4_f64 / v_mfma_f64_4x4x4_4b_f64 (4
+// independent accumulators), and whether f64 MFMA work overlaps VALU f64 FMAs: MODE 0 =
+// MFMA only, 1 = VALU only, 2 = both interleaved in each wave, 3 = half the waves each.
+typedef double d4 __attribute__((ext_vector_type(4)));
+template <int MODE>
+__global__ void k_mm(double* out, double a, double b) {
+  d4 acc0 = {0, 0, 0, 0}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+  double x0 = threadIdx.x * 1e-3, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5,
+         x6 = x0 + 6, x7 = x0 + 7;
+  const double av = a + threadIdx.x * 1e-9;
+  const bool mm = MODE == 0 || MODE == 2 || (MODE == 3 && (threadIdx.x & 64));
+  const bool vv = MODE == 1 || MODE == 2 || (MODE == 3 && !(threadIdx.x & 64));
+  for (int i = 0; i < ITERS; ++i) {
+    if (mm) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b, acc1, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b, acc2, 0, 0, 0);
+      acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b, acc3, 0, 0, 0);
+    }
+    if (vv) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x0) : "v"(a), "v"(b));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x1) : "v"(a), "v"(b));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x2) : "v"(a), "v"(b));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x3) : "v"(a), "v"(b));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x4) : "v"(a), "v"(b));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x5) : "v"(a), "v"(b));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x6) : "v"(a), "v"(b));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x7) : "v"(a), "v"(b));
+      }
+    }
+  }
+  const d4 s = acc0 + acc1 + acc2 + acc3;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s.x + s.y + s.z + s.w + x0 + x1 + x2 + x3 + x4 + x5 + x6 + x7;
+}
+__global__ void k_mm4(double* out, double a, double b) {
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const double av = a + threadIdx.x * 1e-9;
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = __builtin_amdgcn_mfma_f64_4x4x4f64(av, b, acc[u], 0, 0, 0);
+  }
+  double s = 0;
+  for (int u = 0; u < 8; ++u) s += acc[u];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 // Clock: s_memtime ticks per s_memrealtime tick (100 MHz) over a long spin.
 __global__ void k_clock(unsigned long long* out) {
   unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -194,6 +243,28 @@ int main() {
       const double wi = (double)blocks * threads / 64 * ITERS * 32 / (cus * 4.0);
       const double cyc = ms * 1e-3 * ghz * 1e9 / (wi * t.per);
       if (rep == 1) printf("%-34s %8.3f ms  %6.2f cycles per wave-instruction per SIMD\n", t.n, ms, cyc);
+    }
+  }
+  {
+    const double wpsimd = (double)blocks * threads / 64 / (cus * 4.0);  // waves per SIMD
+    struct M { const char* n; void (*k)(double*, double, double); double mf, va; };
+    // per wave: MFMA count, VALU f64 FMA count (MODE 3: half the waves each)
+    M ms[] = {{"mfma16 only (4/iter)", k_mm<0>, 4, 0}, {"fma64 only (32/iter)", k_mm<1>, 0, 32},
+              {"mfma16 + fma64 in each wave", k_mm<2>, 4, 32}, {"half waves mfma16, half fma64", k_mm<3>, 2, 16},
+              {"mfma_f64_4x4x4 only (8/iter)", k_mm4, 8, 0}};
+    for (int rep = 0; rep < 2; ++rep) {
+      for (auto& t : ms) {
+        hipEventRecord(e0);
+        hipLaunchKernelGGL(t.k, dim3(blocks), dim3(threads), 0, 0, d, 0.999, 1e-3);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float msv;
+        hipEventElapsedTime(&msv, e0, e1);
+        const double cyc = msv * 1e-3 * ghz * 1e9;  // per SIMD
+        if (rep == 1)
+          printf("%-34s %8.3f ms  %9.0f cycles per SIMD; %.2f cycles per MFMA if alone, %.2f per fma64 if alone\n",
+                 t.n, msv, cyc, t.mf ? cyc / (wpsimd * ITERS * t.mf) : 0.0, t.va ? cyc / (wpsimd * ITERS * t.va) : 0.0);
+      }
     }
   }
   return 0;
