@@ -135,6 +135,11 @@ struct Geo {
   static constexpr int PF = N <= 256 ? 1 : N <= 1024 ? 2 : 0;  // measured best per N
 #endif
   static constexpr bool PREFETCH = PF != 0;
+#ifdef MGX_MIXFORM
+  static constexpr int MIX = MGX_MIXFORM;
+#else
+  static constexpr int MIX = N == 1024 ? 0 : 1;  // bfly_mixed_tame
+#endif
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
 
@@ -316,16 +321,32 @@ __device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf 
 
 // The mixed pair of a frame whose samples are all finite and below 2^50 in magnitude
 // (no infinity can arise in the FFT). One form serves both lane kinds, with per-lane
-// coefficients (b, c0) from the plan's mixed table (entry a = la | rp of the stage):
-//   generic lanes (b = f_x, c0 = S f_y):  lo = (S fma(f_x, Rr, Lr) - c0 Ri, S fma(f_x, Ri, Li) + c0 Rr),
-//                                         hi = (S fma(-f_x, Rr, Lr) + c0 Ri, -S fma(-f_x, Ri, Li) + c0 Rr);
-//   block-start lanes (b = 1, c0 = 0): t1 = L0 + R0 and t3 = L0 - R0 exactly as jsfft,
-//     lo = (S t1, S t3), hi = (S (Lh + f_x Rh), S f_y Rh) with f = f_{w/2} (fw: lane-uniform
-//     (f_x, S f_y)): the two middle outputs swap places.
-// 11 f64 operations and 6 selects, against 15 and 8 for evaluating both forms (bfly_mixed);
-// the c0 products are 0 x R on block-start lanes, which is why R must be finite.
-__device__ __forceinline__ void bfly_mixed_tame(float2& lo, float2& hi, GTw twm, int idx, double2 fw, bool sp) {
-  const double2 m = ld_tw(twm, idx);
+// coefficients (b, c0, t4, kL) from the plan's mixed table (entry a = la | rp of the stage,
+// two double2 per entry):
+//   generic lanes (b = f_x, c0 = S f_y, t4 = S f_x, kL = -S):
+//     lo = (S fma(f_x, Rr, Lr) - c0 Ri, S fma(f_x, Ri, Li) + c0 Rr),
+//     hi = (S fma(-f_x, Rr, Lr) + c0 Ri, t4 Ri + (kL Li + c0 Rr));
+//   block-start lanes (b = 1, c0 = 0, t4 = S f_y(w/2), kL = 0): t1 = L0 + R0 and
+//     t3 = L0 - R0 exactly as jsfft, lo = (S t1, S t3), hi = (S (Lh + f_x Rh), S f_y Rh)
+//     with f = f_{w/2} (fwx: lane-uniform f_x): the two middle outputs swap places.
+// 10 f64 operations and 4 selects (2 of them per stage, shared by the stage's pairs);
+// the c0 and kL products are 0 x finite on block-start lanes, which is why L, R must be finite.
+__device__ __forceinline__ void bfly_mixed_tame(float2& lo, float2& hi, double2 m, double2 k, double fwx, bool sp) {
+  const double b2 = sp ? fwx : m.x;
+  const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+  const double ui = m.y * Ri, ur = m.y * Rr;
+  const float o1 = (float)__builtin_fma(kS, __builtin_fma(m.x, Rr, Lr), -ui);
+  const float o3 = (float)__builtin_fma(kS, __builtin_fma(-m.x, Rr, Lr), ui);
+  const float o2 = (float)__builtin_fma(kS, __builtin_fma(b2, Ri, Li), ur);
+  const float o4 = (float)__builtin_fma(k.x, Ri, __builtin_fma(k.y, Li, ur));
+  lo.x = o1;
+  lo.y = sp ? o3 : o2;
+  hi.x = sp ? o2 : o3;
+  hi.y = o4;
+}
+// The same pair with the last output selected per lane (S f_y(w/2) Ri on block-start
+// lanes): 11 f64 operations and 6 selects, no (t4, kL) — cheaper for a stage's only pair.
+[[maybe_unused]] __device__ __forceinline__ void bfly_mixed_tame1(float2& lo, float2& hi, double2 m, double2 fw, bool sp) {
   const double b2 = sp ? fw.x : m.x;
   const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
   const double ui = m.y * Ri, ur = m.y * Rr;
@@ -338,6 +359,11 @@ __device__ __forceinline__ void bfly_mixed_tame(float2& lo, float2& hi, GTw twm,
   hi.x = sp ? o2 : o3;
   hi.y = (float)o4;
 }
+
+// How the tame mixed pairs of a stage get (t4, kL) (Geo<N>::MIX): 0 = per pair
+// (bfly_mixed_tame1), 1 = from the plan table, 2 = computed once per stage (t4 = S b,
+// kL = -S; block start: S f_y(w/2), 0). Measured (all features): the table form is 1 % faster
+// at N = 512 and 3 % at N = 2048, 1.8 % slower at N = 1024 (128 VGPRs), where form 0 stays.
 
 // One radix-2 stage on location bit q = q0(P) + I, entirely in registers.
 template <int N, int P, int I, bool FAITH, bool TAME>
@@ -358,7 +384,21 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
       else bfly_generic<FAITH, true>(v[r], v[hi], tw, twf, mask + rp);
 #ifndef MGX_ABL_BRANCH
     } else if (rp == 0) {
-      if constexpr (FAITH && TAME) bfly_mixed_tame(v[r], v[hi], twm, mask + la, ld_tw_u(twm, fidx), la == 0);
+      if constexpr (FAITH && TAME) {
+        // every mixed pair of the stage has rp == 0: one coefficient entry per lane and stage
+        constexpr int npairs = G::R >> (I + 1);
+        const bool sp = la == 0;
+        const double2 fw = ld_tw_u(twm, 2 * fidx);
+        const double2 m = ld_tw(twm, 2 * (mask + la));
+        if constexpr (G::MIX == 0 || (G::MIX == 2 && npairs == 1)) {
+          bfly_mixed_tame1(v[r], v[hi], m, fw, sp);
+        } else if constexpr (G::MIX == 1) {
+          bfly_mixed_tame(v[r], v[hi], m, ld_tw(twm, 2 * (mask + la) + 1), fw.x, sp);
+        } else {
+          const double2 k = make_double2(sp ? fw.y : kS * m.x, sp ? 0.0 : -kS);
+          bfly_mixed_tame(v[r], v[hi], m, k, fw.x, sp);
+        }
+      }
       else bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, fidx, la == 0);
 #else
     } else if (rp == 0) {

@@ -20,7 +20,7 @@ struct DevTables {
   const float* window;       // N, the selected window (src/meyda.js:116-138)
   const double2* tw;         // N/2 - 1 faithful twiddles, stage q at offset 2^q - 1
   const float2* twf;         // same, float32 (MGX_PRECISION_FAST)
-  const double2* twm;        // like tw: (b, c0) per slot pair of the mixed butterflies (plan.cpp mixed_coeffs)
+  const double2* twm;        // like tw, two per entry: (b, c0), (t4, kL) of the mixed butterflies (plan.cpp mixed_coeffs)
   const int* klist;          // N/2: slot location -> spectrum bin
   const int* bblim;          // 25 bark band limits (loudness.js:24-45)
   const uint32_t* mel_rec;   // 64 per-lane records of the mel segment tables (plan.cpp mel_lane_tables)

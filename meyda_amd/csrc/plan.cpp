@@ -160,7 +160,8 @@ void mixed_coeffs(int n, std::vector<double>& tm) {
   const int L = n / 2;
   int stages = 0;
   for (int w = 2; w <= L; w <<= 1) ++stages;
-  tm.assign(2 * (size_t)(L - 1 + stages), 0.0);
+  // 4 doubles per entry: (b, c0, t4, kL) (kernels.hip bfly_mixed_tame)
+  tm.assign(4 * (size_t)(L - 1 + stages), 0.0);
   size_t off = 0;
   for (int w = 2; w <= L; w <<= 1) {
     const int h = w / 2;
@@ -176,14 +177,18 @@ void mixed_coeffs(int n, std::vector<double>& tm) {
     }
     std::vector<int> kl;
     klist(w, kl);
-    tm[2 * off] = 1.0;
+    // block start: b = 1, c0 = 0, t4 = S f_y(w/2), kL = 0
+    tm[4 * off] = 1.0;
+    tm[4 * off + 2] = kJsSqrt1_2 * fi[w / 2];
     for (int a = 1; a < h; a++) {
-      tm[2 * (off + a)] = fr[kl[a]];
-      tm[2 * (off + a) + 1] = kJsSqrt1_2 * fi[kl[a]];
+      tm[4 * (off + a)] = fr[kl[a]];
+      tm[4 * (off + a) + 1] = kJsSqrt1_2 * fi[kl[a]];
+      tm[4 * (off + a) + 2] = kJsSqrt1_2 * fr[kl[a]];
+      tm[4 * (off + a) + 3] = -kJsSqrt1_2;
     }
     const size_t fq = (size_t)(L - 1) + (size_t)(__builtin_ctz((unsigned)w) - 1);
-    tm[2 * fq] = fr[w / 2];
-    tm[2 * fq + 1] = kJsSqrt1_2 * fi[w / 2];
+    tm[4 * fq] = fr[w / 2];
+    tm[4 * fq + 1] = kJsSqrt1_2 * fi[w / 2];
     off += h;
   }
 }
