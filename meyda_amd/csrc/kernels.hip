@@ -135,6 +135,11 @@ struct Geo {
   static constexpr int PF = N <= 256 ? 1 : N <= 1024 ? 2 : 0;  // measured best per N
 #endif
   static constexpr bool PREFETCH = PF != 0;
+#ifdef MGX_LPREMAT
+  static constexpr bool LPREMAT = MGX_LPREMAT;
+#else
+  static constexpr bool LPREMAT = N == 2048;  // measured: N = 2048 1 % faster, N = 256 7 % slower
+#endif
 #ifdef MGX_MIXFORM
   static constexpr int MIX = MGX_MIXFORM;
 #else
@@ -880,14 +885,20 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     GTw tw = gbl(ap->t.tw);
     GTwf twf = gbl(ap->t.twf);
     GTw twm = gbl(ap->t.twm);
+    // G::LPREMAT: the lane parts are recomputed from the lane id in each frame (a few bit
+    // operations) instead of being kept live across the frame loop, where the allocator
+    // spilled them and reloaded from scratch in the middle of the FFT (a vector-memory wait).
+    int lpf[G::NPASS];
+#pragma unroll
+    for (int p = 0; p < G::NPASS; ++p) lpf[p] = G::LPREMAT ? PG::lanepart(p, opaque(lane)) : lp[p];
 #ifndef MGX_ABL_NO_PASSES
     if constexpr (FAITH) {
       // pass 0 has no mixed pairs; the later passes take the tame form when they can
-      run_stages<N, 0, 0, FAITH, false>(v, lp[0], tw, twf, twm);
-      if (tame) run_passes<N, 1, FAITH, true>(v, lp, buf, tw, twf, twm);
-      else run_passes<N, 1, FAITH, false>(v, lp, buf, tw, twf, twm);
+      run_stages<N, 0, 0, FAITH, false>(v, lpf[0], tw, twf, twm);
+      if (tame) run_passes<N, 1, FAITH, true>(v, lpf, buf, tw, twf, twm);
+      else run_passes<N, 1, FAITH, false>(v, lpf, buf, tw, twf, twm);
     } else {
-      run_passes<N, 0, FAITH, false>(v, lp, buf, tw, twf, twm);
+      run_passes<N, 0, FAITH, false>(v, lpf, buf, tw, twf, twm);
     }
 #endif
     const bool want_cplx = ap->out.complex_real != nullptr;
@@ -1050,7 +1061,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
   }
   if (lane < kBark) {
-    rec.band[lane] = pbuf[pd(klim[lane + 1])] - pbuf[pd(klim[lane])];  // limits staged in LDS
+    const int lb = opaque(lane);  // (an address kept live across the frame loop spills at N = 2048)
+    rec.band[lb] = pbuf[pd(klim[lb + 1])] - pbuf[pd(klim[lb])];  // limits staged in LDS
   }
   if (lane == 0) {
     rec.S[0] = total;
