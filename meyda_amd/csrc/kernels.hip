@@ -205,7 +205,11 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+__device__ __forceinline__ double2 ld_tw_u(GTw p, int i);
 __device__ __forceinline__ double2 ld_tw(GTw p, int i) {
+#ifdef MGX_ABL_TWUNI
+  return ld_tw_u(p, __builtin_amdgcn_readfirstlane(i));  // timing ablation: scalar twiddle loads
+#endif
 #ifdef MGX_ABL_TWCONST
   return make_double2((double)i * 1e-3, 0.7);  // timing ablation: no twiddle loads
 #endif
