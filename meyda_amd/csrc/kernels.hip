@@ -532,22 +532,24 @@ __device__ __forceinline__ float slot_amp(float re, float im) {
 // The same amplitude through the f32 hardware reciprocal square root plus one f64 Heron
 // correction (about half the issue cycles: v_rsq_f64 alone costs 16 cycles per wave, the
 // f64 Newton chain 9 more f64 operations). s = re^2 + im^2 exactly as above; q = rsq(s) in
-// f32, y = s q (~2^-22 relative), then g = y + (s - y^2) q / 2 in f64 (~2^-43 relative),
-// rounded to float32: equal to the correctly rounded sqrt unless sqrt(s) lies within 2^-43
-// of a float32 rounding boundary (~2^-19 of the bins; those move by one ulp). ok is false
-// when s leaves [2^-120, 2^120] (0, denormal-range, huge, inf, NaN): the caller then redoes
-// the wave's frame with slot_amp.
+// f32, y = s q (~2^-22 relative), r = s - y^2 exactly in f64, then g = y + r q / 2 as one
+// float32 FMA of (float)r (~2^-43 relative before its single rounding): equal to the
+// correctly rounded sqrt unless sqrt(s) lies within 2^-43 of a float32 rounding boundary
+// (~2^-19 of the bins; those move by one ulp). ok is false when s leaves [2^-80, 2^120]
+// (0, tiny -- where r would be a float32 denormal --, huge, inf, NaN): the caller then
+// redoes the wave's frame with slot_amp.
 __device__ __forceinline__ float slot_amp_rsq(float re, float im, bool& ok) {
   const double xr = re, xi = im;
   const double s = __builtin_fma(xr, xr, xi * xi);
   const float sf = (float)s;
   const float q = __builtin_amdgcn_rsqf(sf);
-  const double y = (double)(sf * q);
-  const double r = __builtin_fma(-y, y, s);
-  const float a = (float)__builtin_fma(r, (double)(0.5f * q), y);
-  // s in [2^-120, 2^120] <=> a in [2^-60, 2^60] (outside, the rsq seed is a denormal, 0,
+  const float yf = sf * q;
+  const double y = yf;
+  const float r = (float)__builtin_fma(-y, y, s);
+  const float a = __builtin_fmaf(r, 0.5f * q, yf);
+  // s in [2^-80, 2^120] <=> a in [2^-40, 2^60] (outside, the rsq seed is a denormal, 0,
   // inf or NaN and so is a, or a is out of range): float32 compares instead of f64 ones
-  ok = a >= 0x1p-60f && a <= 0x1p60f;
+  ok = a >= 0x1p-40f && a <= 0x1p60f;
   return a;
 }
 
@@ -996,10 +998,14 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       T3 = __builtin_fma((double)(jj * jj * jj), ad, T3);
       T4 = __builtin_fma((double)(jj * jj * jj * jj), ad, T4);
     }
-    l2f += __builtin_amdgcn_logf(av[jj]);  // the bare v_log_f32: == log2f for normal inputs
   }
-  // v_log_f32 flushes a denormal input to 0 (-inf). A wave whose sum is not finite (a
-  // zero, denormal, infinite or NaN amplitude; rare) recomputes with log2f's scaling.
+  // sum log2 a by pairs, log2(a_j a_{j+1}) with the bare v_log_f32 (== log2f for normal
+  // inputs; one hardware log per two bins, and the product's rounding is ~2^-24 relative,
+  // finer than the log's own ulp). v_log_f32 flushes a denormal input to 0 (-inf): a wave
+  // whose sum is not finite (a zero, tiny, infinite or NaN amplitude, or a pair product
+  // leaving the normal range; rare) recomputes bin by bin with log2f's scaling.
+#pragma unroll
+  for (int jj = 0; jj < R; jj += 2) l2f += __builtin_amdgcn_logf(av[jj] * av[jj + 1]);
   if (__ballot(!(__builtin_fabsf(l2f) < __builtin_huge_valf()))) {
     l2f = 0.0f;
 #pragma unroll
@@ -1015,11 +1021,14 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // per SIMD) five DPP wave sums measured faster.
   constexpr bool kMomLds = G::MOM_LDS;
   constexpr int MS = G::MOM_STRIDE;
-  const double bb = (double)(R * lane), b2 = bb * bb, b3 = b2 * bb, b4 = b3 * bb;
-  const double P1 = __builtin_fma(bb, T0, T1);
-  const double P2 = T2 + 2.0 * bb * T1 + b2 * T0;
-  const double P3 = T3 + 3.0 * bb * T2 + 3.0 * b2 * T1 + b3 * T0;
-  const double P4 = T4 + 4.0 * bb * T3 + 6.0 * b2 * T2 + 4.0 * b3 * T1 + b4 * T0;
+  // P_p = sum_j (b + j)^p a_j = sum_m C(p, m) b^(p-m) T_m by a Taylor shift (c_i += b c_{i-1},
+  // four sweeps: 10 FMAs; every term is non-negative, so nothing cancels)
+  const double bb = (double)(R * lane);
+  double P1 = T1, P2 = T2, P3 = T3, P4 = T4;
+  P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3); P2 = __builtin_fma(bb, P1, P2); P1 = __builtin_fma(bb, T0, P1);
+  P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3); P2 = __builtin_fma(bb, P1, P2);
+  P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3);
+  P4 = __builtin_fma(bb, P3, P4);
   if constexpr (kMomLds) {
     mom[0 * MS + lane] = P1;
     mom[1 * MS + lane] = P2;

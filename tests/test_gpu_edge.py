@@ -77,6 +77,12 @@ def edge_frames(n):
     y = np.zeros(n, np.float32); y[0] = -0.0; y[1] = 0.0; fr.append(y)          # signed zeros
     fr.append(np.full(n, 1e-45, np.float32))                          # smallest denormal, DC
     y = x.copy(); y[: n // 2] = 0; fr.append(y)                       # half silence
+    # tiny spectra on both sides of the amplitude fast path's range (|X| ~ 2^-40), down to
+    # power spectra at the bottom of the normal float32 range; at 1e-24 the powers are 0.
+    # (Between those, denormal powers leave the reference's own mel sums a few significant
+    # bits: no parity target.)
+    for scale in (1e-9, 1e-13, 1e-16, 1e-24):
+        fr.append((x * np.float32(scale)).astype(np.float32))
     return np.stack(fr)
 
 

@@ -5,6 +5,7 @@ C2: 65,536 x N=512, amplitudeSpectrum + spectralCentroid
 C3: 262,144 x N=1024, spectral* + loudness (+ perceptual)
 C4: 262,144 x N=1024, 40-band mel + 13-coefficient MFCC
 C5: 262,144 x N=2048 per GPU (the 8-GPU config's shard), all features incl. MFCC
+C34-tone: the bench workload (all features, N=1024) on a 440 Hz tone + noise
 Bytes per frame follow SURVEY.md §8(d): 4N in + 4 bytes per output float.
 """
 import json
@@ -25,13 +26,27 @@ CONFIGS = {
                out_floats=7 + 25 + 2, mel=26),
     "C4": dict(n=1024, F=262144, feats=["mfcc"], out_floats=13, mel=40),
     "C5": dict(n=2048, F=262144, feats=capi.ALL_FEATURES, out_floats=50, mel=26),
+    # SURVEY §8(d) sanity variant: the bench workload on a tone + noise signal instead of
+    # uniform noise (data-dependent paths: range checks, small bins)
+    "C34-tone": dict(n=1024, F=262144, feats=capi.ALL_FEATURES, out_floats=50, mel=26, tone=True),
 }
+
+
+def tone_frames(frames, n):
+    """0.5 sin(2 pi 440 t / 44100) over the whole stream, plus 1e-2 x the seeded noise."""
+    F = frames.shape[0]
+    t = torch.arange(n, device=frames.device, dtype=torch.float64)[None, :]
+    t = t + torch.arange(F, device=frames.device, dtype=torch.float64)[:, None] * n
+    sig = 0.5 * torch.sin(2 * torch.pi * 440.0 * t / 44100.0)
+    frames.mul_(1e-2).add_(sig.to(torch.float32))
 
 
 def run(name, cfg, reps=20):
     n, F = cfg["n"], cfg["F"]
     frames = torch.empty(F, n, dtype=torch.float32, device="cuda")
     capi.synth_frames_device(frames, SEED)
+    if cfg.get("tone"):
+        tone_frames(frames, n)
     plan = capi.Plan(buffer_size=n, num_mel_bands=cfg["mel"])
     _, o = plan.alloc_outputs(F, cfg["feats"])
     s = torch.cuda.current_stream()
