@@ -101,10 +101,13 @@ struct Geo {
 #ifndef MGX_WPE1024
 #define MGX_WPE1024 4
 #endif
+#ifndef MGX_WPE512
+#define MGX_WPE512 4
+#endif
 #ifdef MGX_WPE2048
-  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? 4 : N <= 1024 ? MGX_WPE1024 : MGX_WPE2048;
+  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? MGX_WPE512 : N <= 1024 ? MGX_WPE1024 : MGX_WPE2048;
 #else
-  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? 4 : N <= 1024 ? MGX_WPE1024 : 3;
+  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? MGX_WPE512 : N <= 1024 ? MGX_WPE1024 : 3;
 #endif
   // Slot buffer entries (8 bytes): the padded exchange image, the natural-order half
   // spectrum X[0..L] (complex output), the padded prefix row (pd) and the mel scratch.
@@ -143,7 +146,7 @@ struct Geo {
 #ifdef MGX_MIXFORM
   static constexpr int MIX = MGX_MIXFORM;
 #else
-  static constexpr int MIX = N == 1024 ? 0 : 1;  // bfly_mixed_tame
+  static constexpr int MIX = 1;  // bfly_mixed_tame (form 0 was faster at N = 1024 at 128 live VGPRs)
 #endif
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
@@ -388,7 +391,8 @@ __device__ __forceinline__ void bfly_mixed_tame(float2& lo, float2& hi, double2 
 // How the tame mixed pairs of a stage get (t4, kL) (Geo<N>::MIX): 0 = per pair
 // (bfly_mixed_tame1), 1 = from the plan table, 2 = computed once per stage (t4 = S b,
 // kL = -S; block start: S f_y(w/2), 0). Measured (all features): the table form is 1 % faster
-// at N = 512 and 3 % at N = 2048, 1.8 % slower at N = 1024 (128 VGPRs), where form 0 stays.
+// at N = 512, 3 % at N = 2048 and 1.9 % at N = 1024 (there only once the moment and
+// amplitude changes had freed registers; before, 1.8 % slower).
 
 // One radix-2 stage on location bit q = q0(P) + I, entirely in registers.
 template <int N, int P, int I, bool FAITH, bool TAME>
