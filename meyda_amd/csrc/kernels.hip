@@ -209,6 +209,29 @@ __device__ __forceinline__ void prio_lo() {
   if constexpr ((MGX_PRIOSET & REGION) != 0) __builtin_amdgcn_s_setprio(0);
 }
 
+// pa(spectrum bin) of each register after the last pass, live across the whole frame loop:
+// two 16-bit entries per VGPR (MGX_KLPACK=0: one int per register; packed measured 1 %
+// faster at N = 512, 0.2 % at 1024).
+#ifndef MGX_KLPACK
+#define MGX_KLPACK 1
+#endif
+template <int N>
+struct KlTab {
+  static constexpr int R = N / 128;
+#if MGX_KLPACK
+  uint32_t w[R / 2];
+  __device__ __forceinline__ void set(int r, int v) {
+    if (r & 1) w[r >> 1] |= (uint32_t)v << 16;
+    else w[r >> 1] = (uint32_t)v;
+  }
+  __device__ __forceinline__ int operator()(int r) const { return (int)((w[r >> 1] >> (16 * (r & 1))) & 0xFFFFu); }
+#else
+  int w[R];
+  __device__ __forceinline__ void set(int r, int v) { w[r] = v; }
+  __device__ __forceinline__ int operator()(int r) const { return w[r]; }
+#endif
+};
+
 // Wave-level LDS ordering (no global-memory fence: in-flight prefetch loads stay in flight).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -801,7 +824,7 @@ __device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av
 // One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
 template <int N, bool FAITH, bool LITERAL>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
-                                             int lane, const int (&lp)[Geo<N>::NPASS], const int (&kl)[Geo<N>::R],
+                                             int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
                                              const int* klim, float (&xn)[Geo<N>::PREFETCH ? Geo<N>::CH : 1],
                                              GF next) {
@@ -968,7 +991,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
           buf[0] = make_float2(v[r].x, 0.0f);
           buf[L] = make_float2(v[r].y, 0.0f);
         } else {
-          buf[kl[r] - 4 * (kl[r] / 68)] = v[r];  // kl holds pa(bin)
+          buf[kl(r) - 4 * (kl(r) / 68)] = v[r];  // kl holds pa(bin)
         }
       }
       wave_sync();
@@ -986,7 +1009,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
     prio_hi<2>();
 #pragma unroll
-    for (int r = 0; r < R; ++r) amp[kl[r]] = ar[r];  // kl[r] = pa(bin)
+    for (int r = 0; r < R; ++r) amp[kl(r)] = ar[r];  // kl(r) = pa(bin)
   }
   wave_sync();
 
@@ -1235,11 +1258,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   int lp[G::NPASS];
 #pragma unroll
   for (int p = 0; p < G::NPASS; ++p) lp[p] = PG::lanepart(p, lane);
-  int kl[R];  // spectrum bin held by each register after the last pass
+  KlTab<N> kl;  // spectrum bin held by each register after the last pass
   {
     const auto klist = gbl(ap->t.klist);
 #pragma unroll
-    for (int r = 0; r < R; ++r) kl[r] = pa(klist[lp[G::NPASS - 1] | PG::rpart(G::NPASS - 1, r)]);
+    for (int r = 0; r < R; ++r) kl.set(r, pa(klist[lp[G::NPASS - 1] | PG::rpart(G::NPASS - 1, r)]));
   }
   const bool dc_lane = lp[G::NPASS - 1] == 0;
 
