@@ -822,7 +822,7 @@ __device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av
 }
 
 // One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
-template <int N, bool FAITH, bool LITERAL>
+template <int N, bool FAITH, bool LITERAL, bool SUB>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
                                              int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
@@ -1033,30 +1033,40 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) av[jj] = amp[pa(R * lane + jj)];
   prio_lo<2>();
+  // The moment and log sums only when a feature reads them (need_mom); the amplitude total
+  // T0 always (S0, rolloff, the non-finite test). SUB: a feature subset, the flags are read
+  // at run time; otherwise every feature is requested and the branches compile away (the
+  // all-feature kernel keeps its schedule: run-time branches there cost 0.7 %).
+  const bool need_mom = SUB ? (bool)ap->need_mom : true;
   double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
   float l2f = 0.0f;
+  if (need_mom) {
 #pragma unroll
-  for (int jj = 0; jj < R; ++jj) {
-    const double ad = av[jj];
-    T0 += ad;
-    if (jj > 0) {
-      T1 = __builtin_fma((double)jj, ad, T1);
-      T2 = __builtin_fma((double)(jj * jj), ad, T2);
-      T3 = __builtin_fma((double)(jj * jj * jj), ad, T3);
-      T4 = __builtin_fma((double)(jj * jj * jj * jj), ad, T4);
+    for (int jj = 0; jj < R; ++jj) {
+      const double ad = av[jj];
+      T0 += ad;
+      if (jj > 0) {
+        T1 = __builtin_fma((double)jj, ad, T1);
+        T2 = __builtin_fma((double)(jj * jj), ad, T2);
+        T3 = __builtin_fma((double)(jj * jj * jj), ad, T3);
+        T4 = __builtin_fma((double)(jj * jj * jj * jj), ad, T4);
+      }
     }
-  }
-  // sum log2 a by pairs, log2(a_j a_{j+1}) with the bare v_log_f32 (== log2f for normal
-  // inputs; one hardware log per two bins, and the product's rounding is ~2^-24 relative,
-  // finer than the log's own ulp). v_log_f32 flushes a denormal input to 0 (-inf): a wave
-  // whose sum is not finite (a zero, tiny, infinite or NaN amplitude, or a pair product
-  // leaving the normal range; rare) recomputes bin by bin with log2f's scaling.
+    // sum log2 a by pairs, log2(a_j a_{j+1}) with the bare v_log_f32 (== log2f for normal
+    // inputs; one hardware log per two bins, and the product's rounding is ~2^-24 relative,
+    // finer than the log's own ulp). v_log_f32 flushes a denormal input to 0 (-inf): a wave
+    // whose sum is not finite (a zero, tiny, infinite or NaN amplitude, or a pair product
+    // leaving the normal range; rare) recomputes bin by bin with log2f's scaling.
 #pragma unroll
-  for (int jj = 0; jj < R; jj += 2) l2f += __builtin_amdgcn_logf(av[jj] * av[jj + 1]);
-  if (__ballot(!(__builtin_fabsf(l2f) < __builtin_huge_valf()))) {
-    l2f = 0.0f;
+    for (int jj = 0; jj < R; jj += 2) l2f += __builtin_amdgcn_logf(av[jj] * av[jj + 1]);
+    if (__ballot(!(__builtin_fabsf(l2f) < __builtin_huge_valf()))) {
+      l2f = 0.0f;
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) l2f += log2f(av[jj]);
+      for (int jj = 0; jj < R; ++jj) l2f += log2f(av[jj]);
+    }
+  } else {
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) T0 += (double)av[jj];
   }
   wave_sync();  // every lane has read the amplitude row: the buffer takes the prefix sums next
   FrameRec& rec = recs[fb];
@@ -1076,7 +1086,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3); P2 = __builtin_fma(bb, P1, P2);
   P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3);
   P4 = __builtin_fma(bb, P3, P4);
-  if constexpr (kMomLds) {
+  if (kMomLds && need_mom) {
     mom[0 * MS + lane] = P1;
     mom[1 * MS + lane] = P2;
     mom[2 * MS + lane] = P3;
@@ -1090,12 +1100,15 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // spectralRolloff.js:6-15: the largest m with P(m) <= 0.99 total (P(0) = 0).
   const double thr = 0.99 * total;
   int cnt = 0;
-  double pk = excl;  // P(R lane + jj), accumulated again rather than kept (registers)
+  const bool need_prefix = SUB ? (bool)ap->need_prefix : true;
+  if (need_prefix) {
+    double pk = excl;  // P(R lane + jj), accumulated again rather than kept (registers)
 #pragma unroll
-  for (int jj = 0; jj < R; ++jj) {
-    pbuf[pd(R * lane + jj)] = pk;
-    cnt += __popcll(__ballot(pk <= thr));
-    pk += (double)av[jj];
+    for (int jj = 0; jj < R; ++jj) {
+      pbuf[pd(R * lane + jj)] = pk;
+      cnt += __popcll(__ballot(pk <= thr));
+      pk += (double)av[jj];
+    }
   }
   const int roll_m = (total > thr) ? cnt - 1 : L;
   // The lane's mel records, then (G::PF == 2) the next frame: issued after the last table
@@ -1106,7 +1119,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   MelTab<N> mt;
   if (ap->need_mfcc) mt.load(ap, lane);
   prefetch_next();
-  if constexpr (!kMomLds) {
+  if (!kMomLds && need_mom) {
 #ifdef MGX_ABL_NOWSUM
     const double S1 = readlane_d(P1, 63), S2 = readlane_d(P2, 63), S3 = readlane_d(P3, 63), S4 = readlane_d(P4, 63);
     const double l2 = readlane_d((double)l2f, 63);
@@ -1120,7 +1133,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       rec.ln2sum = l2;
     }
   }
-  if (lane < kBark) {
+  if (need_prefix && lane < kBark) {
     const int lb = opaque(lane);  // (an address kept live across the frame loop spills at N = 2048)
     rec.band[lb] = pbuf[pd(klim[lb + 1])] - pbuf[pd(klim[lb])];  // limits staged in LDS
   }
@@ -1139,7 +1152,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   } else if (ABL_ON(MELSCAN) && ap->need_mfcc) {
     mel_energies<N>(ap, av, lane, buf, rec, mt);
   }
-  if constexpr (kMomLds) {
+  if (kMomLds && need_mom) {
     wave_sync();
     const int row = lane < 40 ? lane >> 3 : 0;
     const double* src = mom + row * MS + (lane & 7);  // entries g, g+8, ..., g+56 of the row
@@ -1224,7 +1237,7 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   return sc == MGX_RMS ? sqrt(v) : v;
 }
 
-template <int N, bool FAITH, bool LITERAL>
+template <int N, bool FAITH, bool LITERAL, bool SUB>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
@@ -1319,7 +1332,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       } else {
         load(x, b, j);
       }
-      frame_phase1<N, FAITH, LITERAL>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
+      frame_phase1<N, FAITH, LITERAL, SUB>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
                                       reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next);
     }
     wave_sync();
@@ -1493,17 +1506,17 @@ __global__ void pcm_decode_kernel(const unsigned char* __restrict__ pcm, uint64_
   }
 }
 
-template <int N, bool FAITH, bool LITERAL>
+template <int N, bool FAITH, bool LITERAL, bool SUB = false>
 hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
   const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
-  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL>), dim3(grid), dim3(kThreads), lds, stream, a);
+  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB>), dim3(grid), dim3(kThreads), lds, stream, a);
   return hipGetLastError();
 }
 
-template <int N, bool FAITH, bool LITERAL>
+template <int N, bool FAITH, bool LITERAL, bool SUB = false>
 int occupancy_n(size_t lds) {
   int blocks = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL>, kThreads, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL, SUB>, kThreads, lds) !=
       hipSuccess)
     return 0;
   return blocks;
@@ -1514,13 +1527,17 @@ int occupancy_prec(int precision, int mode, int ncoef, int nfilt) {
   const size_t lds = Lds<N>::bytes(ncoef, nfilt);
   if (mode == MGX_MODE_LITERAL) return occupancy_n<N, true, true>(lds);
   if (precision == MGX_PRECISION_FAST) return occupancy_n<N, false, false>(lds);
-  return occupancy_n<N, true, false>(lds);
+  // the grid serves both faithful kernels (all features / a subset)
+  const int a = occupancy_n<N, true, false>(lds), b = occupancy_n<N, true, false, true>(lds);
+  return a < b ? a : b;
 }
 
 template <int N>
 hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, hipStream_t stream) {
   if (mode == MGX_MODE_LITERAL) return launch_n<N, true, true>(a, grid, stream);
   if (precision == MGX_PRECISION_FAST) return launch_n<N, false, false>(a, grid, stream);
+  // a spectral feature subset that skips the moment / prefix work takes the SUB kernel
+  if (a.need_spectrum && !(a.need_mom && a.need_prefix)) return launch_n<N, true, false, true>(a, grid, stream);
   return launch_n<N, true, false>(a, grid, stream);
 }
 

@@ -44,6 +44,8 @@ struct KernelArgs {
   int need_spectrum;     // any spectral output requested
   int need_loudness;     // loudness / perceptual outputs requested
   int need_mfcc;
+  int need_mom;          // centroid / flatness / slope / spread / skewness / kurtosis: S1..S4, sum log2 a
+  int need_prefix;       // rolloff or loudness: the prefix row (rolloff count, bark band sums)
 };
 
 // Launchers (kernels.hip).

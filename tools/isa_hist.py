@@ -7,9 +7,10 @@ from collections import Counter
 
 
 def body(path, n=1024, faith=1, lit=0):
-    name = "_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb%dELb%dEEEvNS_10KernelArgsE" % (n, faith, lit)
+    names = ["_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb%dELb%dELb0EEEvNS_10KernelArgsE" % (n, faith, lit),
+             "_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb%dELb%dEEEvNS_10KernelArgsE" % (n, faith, lit)]
     lines = open(path).read().split("\n")
-    start = lines.index(name + ":" + lines[[i for i, l in enumerate(lines) if l.startswith(name + ":")][0]][len(name) + 1:])
+    start = [i for i, l in enumerate(lines) if any(l.startswith(nm + ":") for nm in names)][0]
     out = []
     for l in lines[start + 1:]:
         if l.startswith(".Lfunc_end"):
