@@ -1162,6 +1162,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     t += dpp_d<0x141>(t);  // row_half_mirror: each 8-lane group holds its row's total
     if (lane < 40 && (lane & 7) == 0) (&rec.S[1])[row] = t;  // S[1..4], then ln2sum
   }
+#else
+  prefetch_next();  // (timing ablation: the frames are still read)
 #endif
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
 }
