@@ -160,6 +160,9 @@ SUBSETS = {
     "loudness": ["loudness", "perceptualSharpness"],
     "mfcc_only": ["mfcc"],
     "amp_centroid": ["amplitudeSpectrum", "spectralCentroid"],
+    # the subset kernel's two flags one at a time (kernels.hip SUB: need_prefix, need_mom)
+    "rolloff_only": ["spectralRolloff"],
+    "flatness_slope_mfcc": ["spectralFlatness", "spectralSlope", "mfcc"],
 }
 SCALAR_INDEX = {k: i for i, k in enumerate(SCALARS)}
 
