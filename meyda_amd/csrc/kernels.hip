@@ -232,11 +232,12 @@ struct KlTab {
 #endif
 };
 
-// A frame sample: read once and never again, so a non-temporal load (`nt`). Measured: the
-// HBM-bound time-only features 12 % faster (5.9 TB/s); no change where the kernel is
-// VALU-bound. MGX_NT_FRAMES=0 restores plain loads.
+// A frame sample: read once and never again. MGX_NT_FRAMES=1: non-temporal loads (`nt`).
+// Measured: the HBM-bound time-only features 12 % faster on a 1 GiB batch (5.9 TB/s), but
+// C2's 128 MiB batch 12 % slower (with plain loads it stays resident in the 256 MiB MALL
+// across launches); no change where the kernel is VALU-bound. Plain loads by default.
 #ifndef MGX_NT_FRAMES
-#define MGX_NT_FRAMES 1
+#define MGX_NT_FRAMES 0
 #endif
 __device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))) float* p) {
 #if MGX_NT_FRAMES
