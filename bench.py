@@ -159,13 +159,25 @@ def main():
         bytes_per_frame = 4 * n + 4 * OUT_FLOATS
         achieved = F * bytes_per_frame / (kernel_ms * 1e-3) / 1e9
         traffic = None
+        key = "%s_n%d_f%d" % (args.precision, n, F)
         prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(prof):
             with open(prof) as fh:
                 pj = json.load(fh)
-            key = "%s_n%d_f%d" % (args.precision, n, F)
             if key in pj:
                 traffic = pj[key]["hbm_bytes_per_launch"]
+        # the faithful path is FP64-VALU bound; its instruction mix from the
+        # committed PMC passes (tools/gpu_pmc_cur.sh + tools/pmc_valu_json.py)
+        valu = None
+        prof = os.path.join(ROOT, "profiles", "pmc_valu.json")
+        if os.path.exists(prof):
+            with open(prof) as fh:
+                pv = json.load(fh)
+            if key in pv:
+                v = pv[key]
+                valu = {"instr_per_frame": v["valu_instr_per_frame"], "f64_per_frame": v["f64_instr_per_frame"],
+                        "cvt_per_frame": v["cvt_instr_per_frame"], "est_valu_busy": v["est_valu_busy"],
+                        "est_fp64_cvt_busy": v["est_fp64_pipe_busy"], "source": "profiles/pmc_valu.json"}
         line = {
             "metric": "audio frames/sec (bufferSize=1024, all features) at 1/2/4/8 GPUs; % HBM roofline",
             "value": world * F * args.steps / elapsed,
@@ -188,6 +200,8 @@ def main():
                          "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
                          "bytes_per_frame": bytes_per_frame},
         }
+        if valu:
+            line["valu"] = valu
         if fast:
             line["fast_mode"] = fast
         if not args.no_cpu_baseline and world == 1:

@@ -29,4 +29,6 @@ tail -1 $O/prof_bench.log
 step traffic
 $R/tools/gpu_traffic.sh > $O/traffic.log 2>&1 || { tail -20 $O/traffic.log; exit 1; }
 cp $R/gpurun_out/traffic/summary.json $O/pmc_traffic.json
+step valu_pmc
+$R/tools/gpu_pmc_cur.sh || { echo "pmc failed"; exit 1; }
 step done
