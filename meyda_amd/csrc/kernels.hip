@@ -186,11 +186,17 @@ struct PassGeo {
 
 
 // Bank-padded layouts of the amplitude row (floats) and of its prefix sums (doubles) in
-// the slot buffer: lane l reads/writes R consecutive entries with 16-byte accesses, and
-// 4 floats (2 doubles) of padding per 64 floats (32 doubles) shift each successive group
-// of lanes onto the banks the previous group left free (no 2- or 4-way conflicts).
+// the slot buffer: lane l reads the row (ds_read2_b64) and writes the prefix
+// (ds_write2_b64) as R consecutive entries; both instructions serve 16 consecutive lanes
+// per LDS cycle with banks (a/4) mod 32 (MI355X_MICROARCH.md §LDS). The prefix row's 1
+// double of padding per 16 gives those 16 lanes 16 distinct bank pairs at every R (the
+// former 2 per 32 left 2-way conflicts: 32 extra LDS cycles per frame at N = 1024,
+// SQ_LDS_BANK_CONFLICT). The amplitude row keeps 4 floats per 64 (2-way on its reads): 2
+// per 32 removes those too but changed the surrounding code generation and measured
+// 2.5 % slower; the LDS is not what bounds the kernel.
 __device__ __forceinline__ int pa(int k) { return k + 4 * (k >> 6); }
-__device__ __forceinline__ int pd(int d) { return d + 2 * (d >> 5); }
+__device__ __forceinline__ int pa_inv(int k) { return k - 4 * (k / 68); }  // pa(b) = 68 (b >> 6) + (b & 63)
+__device__ __forceinline__ int pd(int d) { return d + (d >> 4); }
 
 
 // Wave priority around LDS round trips (s_setprio): a wave that reaches an exchange issues
@@ -1006,7 +1012,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
           buf[0] = make_float2(v[r].x, 0.0f);
           buf[L] = make_float2(v[r].y, 0.0f);
         } else {
-          buf[kl(r) - 4 * (kl(r) / 68)] = v[r];  // kl holds pa(bin)
+          buf[pa_inv(kl(r))] = v[r];  // kl holds pa(bin)
         }
       }
       wave_sync();
