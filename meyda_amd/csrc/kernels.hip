@@ -1054,14 +1054,16 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) av[jj] = amp[pa(R * lane + jj)];
   prio_lo<2>();
-  // The moment and log sums only when a feature reads them (need_mom); the amplitude total
-  // T0 always (S0, rolloff, the non-finite test). SUB: a feature subset, the flags are read
-  // at run time; otherwise every feature is requested and the branches compile away (the
-  // all-feature kernel keeps its schedule: run-time branches there cost 0.7 %).
-  const bool need_mom = SUB ? (bool)ap->need_mom : true;
+  // The moment and log sums only as far as a feature reads them (need_mom: 0 none, 1 S1 for
+  // centroid / slope, 2 S1..S4 and sum log2 a); the amplitude total T0 always (S0, rolloff,
+  // the non-finite test). SUB: a feature subset, the flags are read at run time; otherwise
+  // every feature is requested and the branches compile away (the all-feature kernel keeps
+  // its schedule: run-time branches there cost 0.7 %).
+  const int mom_level = SUB ? ap->need_mom : 2;
+  const bool need_mom = mom_level > 0, need_hi = mom_level > 1;
   double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
   float l2f = 0.0f;
-  if (need_mom) {
+  if (need_hi) {
 #pragma unroll
     for (int jj = 0; jj < R; ++jj) {
       const double ad = av[jj];
@@ -1085,6 +1087,13 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #pragma unroll
       for (int jj = 0; jj < R; ++jj) l2f += log2f(av[jj]);
     }
+  } else if (need_mom) {
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) {
+      const double ad = av[jj];
+      T0 += ad;
+      if (jj > 0) T1 = __builtin_fma((double)jj, ad, T1);
+    }
   } else {
 #pragma unroll
     for (int jj = 0; jj < R; ++jj) T0 += (double)av[jj];
@@ -1103,16 +1112,22 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // four sweeps: 10 FMAs; every term is non-negative, so nothing cancels)
   const double bb = (double)(R * lane);
   double P1 = T1, P2 = T2, P3 = T3, P4 = T4;
-  P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3); P2 = __builtin_fma(bb, P1, P2); P1 = __builtin_fma(bb, T0, P1);
-  P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3); P2 = __builtin_fma(bb, P1, P2);
-  P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3);
-  P4 = __builtin_fma(bb, P3, P4);
+  if (need_hi) {
+    P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3); P2 = __builtin_fma(bb, P1, P2); P1 = __builtin_fma(bb, T0, P1);
+    P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3); P2 = __builtin_fma(bb, P1, P2);
+    P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3);
+    P4 = __builtin_fma(bb, P3, P4);
+  } else {
+    P1 = __builtin_fma(bb, T0, P1);
+  }
   if (kMomLds && need_mom) {
     mom[0 * MS + lane] = P1;
-    mom[1 * MS + lane] = P2;
-    mom[2 * MS + lane] = P3;
-    mom[3 * MS + lane] = P4;
-    mom[4 * MS + lane] = (double)l2f;
+    if (need_hi) {
+      mom[1 * MS + lane] = P2;
+      mom[2 * MS + lane] = P3;
+      mom[3 * MS + lane] = P4;
+      mom[4 * MS + lane] = (double)l2f;
+    }
   }
   // prefix P(k) = sum_{i<k} a_i: lane-exclusive offset + local prefix
   const double incl = wave_inclusive_scan(T0);
@@ -1145,8 +1160,12 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     const double S1 = readlane_d(P1, 63), S2 = readlane_d(P2, 63), S3 = readlane_d(P3, 63), S4 = readlane_d(P4, 63);
     const double l2 = readlane_d((double)l2f, 63);
 #else
-    const double S1 = wave_sum(P1), S2 = wave_sum(P2), S3 = wave_sum(P3), S4 = wave_sum(P4);
-    const double l2 = wave_sum((double)l2f);
+    const double S1 = wave_sum(P1);
+    double S2 = 0, S3 = 0, S4 = 0, l2 = 0;
+    if (need_hi) {
+      S2 = wave_sum(P2); S3 = wave_sum(P3); S4 = wave_sum(P4);
+      l2 = wave_sum((double)l2f);
+    }
 #endif
     wave_sync();
     if (lane == 0) {
@@ -1560,7 +1579,7 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
   if (mode == MGX_MODE_LITERAL) return launch_n<N, true, true>(a, grid, stream);
   if (precision == MGX_PRECISION_FAST) return launch_n<N, false, false>(a, grid, stream);
   // a spectral feature subset that skips the moment / prefix work takes the SUB kernel
-  if (a.need_spectrum && !(a.need_mom && a.need_prefix)) return launch_n<N, true, false, true>(a, grid, stream);
+  if (a.need_spectrum && !(a.need_mom == 2 && a.need_prefix)) return launch_n<N, true, false, true>(a, grid, stream);
   return launch_n<N, true, false>(a, grid, stream);
 }
 

@@ -44,7 +44,7 @@ struct KernelArgs {
   int need_spectrum;     // any spectral output requested
   int need_loudness;     // loudness / perceptual outputs requested
   int need_mfcc;
-  int need_mom;          // centroid / flatness / slope / spread / skewness / kurtosis: S1..S4, sum log2 a
+  int need_mom;          // 2: flatness / spread / skewness / kurtosis (S1..S4, sum log2 a); 1: centroid / slope (S1); 0
   int need_prefix;       // rolloff or loudness: the prefix row (rolloff count, bark band sums)
 };
 

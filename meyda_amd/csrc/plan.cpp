@@ -515,9 +515,10 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.need_loudness = o->loudness_specific || o->scalars[MGX_LOUDNESS_TOTAL] || o->scalars[MGX_PERCEPTUAL_SPREAD] ||
                     o->scalars[MGX_PERCEPTUAL_SHARPNESS];
   a.need_mfcc = o->mfcc != nullptr;
-  a.need_mom = o->scalars[MGX_SPECTRAL_CENTROID] || o->scalars[MGX_SPECTRAL_FLATNESS] ||
-               o->scalars[MGX_SPECTRAL_SLOPE] || o->scalars[MGX_SPECTRAL_SPREAD] ||
-               o->scalars[MGX_SPECTRAL_SKEWNESS] || o->scalars[MGX_SPECTRAL_KURTOSIS];
+  // moment sums: 2 = S1..S4 and sum log2 a, 1 = S1 only, 0 = none
+  a.need_mom = (o->scalars[MGX_SPECTRAL_FLATNESS] || o->scalars[MGX_SPECTRAL_SPREAD] ||
+                o->scalars[MGX_SPECTRAL_SKEWNESS] || o->scalars[MGX_SPECTRAL_KURTOSIS]) ? 2
+               : (o->scalars[MGX_SPECTRAL_CENTROID] || o->scalars[MGX_SPECTRAL_SLOPE]) ? 1 : 0;
   a.need_prefix = a.need_loudness || o->scalars[MGX_SPECTRAL_ROLLOFF];
   const uint64_t fb = (uint64_t)mgx::frames_per_batch(p->n);
   const uint64_t nb = (nframes + fb - 1) / fb;
