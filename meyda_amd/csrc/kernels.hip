@@ -906,7 +906,20 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     for (int c = 0; c < CH; ++c) e64 = __builtin_fma((double)x[c], (double)x[c], e64);
     e = wave_sum(e64);
   } else {
+#ifdef MGX_ENERGY_F64SUM
     e = wave_sum((double)e32);
+#else
+    // the 64 lane partials summed in float32 too (6 DPP-fused adds instead of 6 f64 DPP
+    // steps): ~4e-7 relative at most on top of the partials' own ~1e-6, against the 1e-5 bar
+    float t = e32;
+    t += dpp_f<0xB1>(t);
+    t += dpp_f<0x4E>(t);
+    t += dpp_f<0x141>(t);
+    t += dpp_f<0x140>(t);
+    t += dpp_f<0x142, 0xA>(t);
+    t += dpp_f<0x143, 0xC>(t);
+    e = (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
+#endif
   }
   if (lane == 0) {
     recs[fb].energy = e;
