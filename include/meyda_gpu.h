@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MGX_ABI_VERSION 1
+#define MGX_ABI_VERSION 2  /* 2: mgx_extract_host_pcm takes the PCM byte count */
 
 typedef enum mgx_status {
   MGX_OK = 0,
@@ -194,15 +194,17 @@ typedef struct mgx_wav_info {
 int mgx_wav_parse(const void* bytes, uint64_t num_bytes, mgx_wav_info* info);
 
 /* Device decode: `sample_frames` interleaved frames of `channels` samples at
- * `pcm` (device memory) -> float32 samples of channel `channel` at `out`. */
+ * `pcm` (device memory, any byte alignment) -> float32 samples of channel `channel` at `out`. */
 int mgx_pcm_decode_device(const void* pcm, uint64_t sample_frames, uint32_t format, uint32_t channels,
                           uint32_t channel, float* out, void* stream);
 
 /* Host PCM in, host outputs: floor(sample_frames / buffer_size) buffers of channel
  * `channel`. The raw PCM (not float32) crosses PCIe and is decoded on the device;
- * outputs are laid out as for mgx_extract_host. */
-int mgx_extract_host_pcm(mgx_plan* plan, const void* pcm, uint64_t sample_frames, uint32_t format,
-                         uint32_t channels, uint32_t channel, const mgx_outputs* outputs);
+ * outputs are laid out as for mgx_extract_host. `pcm_bytes` is the size of the buffer at
+ * `pcm`: sample_frames * channels * bytes-per-sample beyond it is MGX_E_INVALID_ARGUMENT
+ * (no read past the caller's buffer). `pcm` needs no alignment. */
+int mgx_extract_host_pcm(mgx_plan* plan, const void* pcm, uint64_t pcm_bytes, uint64_t sample_frames,
+                         uint32_t format, uint32_t channels, uint32_t channel, const mgx_outputs* outputs);
 
 int mgx_is_power_of_two(double n);           /* src/utils.js:13-19 */
 int mgx_feature_index(const char* name);     /* -1 if unknown */

@@ -6,6 +6,7 @@
  * Exports:
  *   createPlan(opts)                     -> plan handle (external; destroyed by GC or destroyPlan)
  *   destroyPlan(plan)
+ *   planBusy(plan)                       -> true while an async extraction owns the plan
  *   extract(plan, frames, features)      -> { name: TypedArray }   (synchronous)
  *   extractAsync(plan, frames, features) -> Promise<{ name: TypedArray }>  (napi_async_work)
  *   extractWav(plan, wavBytes, features[, channel]) / extractWavAsync(...)
@@ -43,15 +44,27 @@ static napi_value throw_mgx(napi_env env, int rc) {
 typedef struct {
   mgx_plan* plan;
   mgx_plan_desc desc;
-  int busy;  /* an async extraction owns the plan */
+  int busy;       /* an async extraction owns the plan */
+  int finalized;  /* the JS handle was collected while busy: async_complete frees the box */
 } plan_box;
 
+static void plan_box_free(plan_box* b) {
+  if (b->plan) mgx_plan_destroy(b->plan);
+  free(b);
+}
+
+/* A queued or running async job holds a reference to the plan's external, so the GC
+ * cannot collect it mid-job; `finalized` covers a finalizer that runs anyway while the
+ * job is in flight (environment teardown): the box is then freed by async_complete. */
 static void plan_finalize(napi_env env, void* data, void* hint) {
   (void)env;
   (void)hint;
   plan_box* b = (plan_box*)data;
-  if (b->plan) mgx_plan_destroy(b->plan);
-  free(b);
+  if (b->busy) {
+    b->finalized = 1;
+    return;
+  }
+  plan_box_free(b);
 }
 
 static int get_u32_prop(napi_env env, napi_value obj, const char* name, uint32_t* out) {
@@ -153,6 +166,16 @@ static plan_box* get_plan(napi_env env, napi_value v) {
   return b;
 }
 
+static napi_value plan_busy(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], r;
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  plan_box* b = argc ? get_plan(env, argv[0]) : NULL;
+  if (!b) return NULL;
+  CHECK(napi_get_boolean(env, b->busy != 0, &r));
+  return r;
+}
+
 static napi_value destroy_plan(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -177,6 +200,7 @@ typedef struct {
   uint64_t nframes;
   /* PCM input (extractWav): interleaved samples, decoded on the device */
   const unsigned char* pcm;
+  uint64_t pcm_bytes;
   uint64_t pcm_frames;
   uint32_t pcm_format, pcm_channels, pcm_channel;
   mgx_outputs out;
@@ -184,6 +208,7 @@ typedef struct {
   size_t bytes[NSLOTS];
   int want[NSLOTS];
   napi_ref frames_ref;
+  napi_ref plan_ref;  /* keeps the plan's external alive while the job is queued or running */
   napi_deferred deferred;
   napi_async_work work;
   int rc;
@@ -345,6 +370,7 @@ static int job_prepare_wav(napi_env env, job* j, napi_value wav_v, napi_value fe
     return 0;
   }
   j->pcm = data + wi.data_offset;
+  j->pcm_bytes = wi.data_bytes;
   j->pcm_frames = wi.sample_frames;
   j->pcm_format = wi.pcm_format;
   j->pcm_channels = wi.channels;
@@ -355,7 +381,7 @@ static int job_prepare_wav(napi_env env, job* j, napi_value wav_v, napi_value fe
 
 static void job_run(job* j) {
   if (j->pcm)
-    j->rc = mgx_extract_host_pcm(j->box->plan, j->pcm, j->pcm_frames, j->pcm_format, j->pcm_channels,
+    j->rc = mgx_extract_host_pcm(j->box->plan, j->pcm, j->pcm_bytes, j->pcm_frames, j->pcm_format, j->pcm_channels,
                                  j->pcm_channel, &j->out);
   else
     j->rc = mgx_extract_host(j->box->plan, j->frames, j->nframes, &j->out);
@@ -439,7 +465,8 @@ static void async_execute(napi_env env, void* data) {
 
 static void async_complete(napi_env env, napi_status status, void* data) {
   job* j = (job*)data;
-  j->box->busy = 0;
+  plan_box* box = j->box;
+  box->busy = 0;
   if (status != napi_ok || j->rc) {
     napi_value msg, err;
     napi_create_string_utf8(env, j->rc ? j->err : "async extraction cancelled", NAPI_AUTO_LENGTH, &msg);
@@ -449,9 +476,11 @@ static void async_complete(napi_env env, napi_status status, void* data) {
     napi_resolve_deferred(env, j->deferred, job_result(env, j));
   }
   napi_delete_reference(env, j->frames_ref);
+  napi_delete_reference(env, j->plan_ref);
   napi_delete_async_work(env, j->work);
   job_free_buffers(j);
   free(j);
+  if (box->finalized) plan_box_free(box);
 }
 
 static napi_value extract_async_common(napi_env env, napi_callback_info info, int wav) {
@@ -479,6 +508,7 @@ static napi_value extract_async_common(napi_env env, napi_callback_info info, in
   }
   napi_value promise, name;
   CHECK(napi_create_reference(env, argv[1], 1, &j->frames_ref));  /* keep the input alive */
+  CHECK(napi_create_reference(env, argv[0], 1, &j->plan_ref));    /* and the plan */
   CHECK(napi_create_promise(env, &j->deferred, &promise));
   CHECK(napi_create_string_utf8(env, "meyda_extract", NAPI_AUTO_LENGTH, &name));
   CHECK(napi_create_async_work(env, NULL, name, async_execute, async_complete, j, &j->work));
@@ -606,6 +636,7 @@ static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"createPlan", NULL, create_plan, NULL, NULL, NULL, napi_enumerable, NULL},
       {"destroyPlan", NULL, destroy_plan, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"planBusy", NULL, plan_busy, NULL, NULL, NULL, napi_enumerable, NULL},
       {"extract", NULL, extract_sync, NULL, NULL, NULL, napi_enumerable, NULL},
       {"extractAsync", NULL, extract_async, NULL, NULL, NULL, napi_enumerable, NULL},
       {"extractWav", NULL, extract_wav_sync, NULL, NULL, NULL, napi_enumerable, NULL},

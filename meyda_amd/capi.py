@@ -113,7 +113,7 @@ def lib():
         L.mgx_wav_parse.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(WavInfo)]
         L.mgx_pcm_decode_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
-        L.mgx_extract_host_pcm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+        L.mgx_extract_host_pcm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(Outputs)]
         _lib = L
     return _lib
@@ -252,7 +252,7 @@ class Plan:
         fmt = PCM_FORMATS[fmt] if isinstance(fmt, str) else fmt
         F = sample_frames // self.n
         out, o = self._host_outputs(F, features)
-        check(lib().mgx_extract_host_pcm(self._h, buf.ctypes.data, sample_frames, fmt, channels, channel,
+        check(lib().mgx_extract_host_pcm(self._h, buf.ctypes.data, buf.size, sample_frames, fmt, channels, channel,
                                          ctypes.byref(o)))
         return out
 

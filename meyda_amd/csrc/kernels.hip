@@ -1544,18 +1544,20 @@ __global__ void pcm_decode_kernel(const unsigned char* __restrict__ pcm, uint64_
                                   uint32_t stride, uint32_t offset, float* __restrict__ out) {
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += step) {
+    // samples are assembled from bytes: a caller's device pointer need not be aligned
     const unsigned char* b = pcm + i * stride + offset;
+    auto w32 = [b]() { return (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24; };
     float v;
     switch (format) {
-      case MGX_PCM_S16: v = (float)*reinterpret_cast<const int16_t*>(b) * (1.0f / 32768.0f); break;
+      case MGX_PCM_S16: v = (float)(int16_t)(uint16_t)((uint32_t)b[0] | (uint32_t)b[1] << 8) * (1.0f / 32768.0f); break;
       case MGX_PCM_U8: v = (float)((int)b[0] - 128) * (1.0f / 128.0f); break;
       case MGX_PCM_S24: {
         const int32_t u = (int32_t)((uint32_t)b[0] << 8 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 24) >> 8;
         v = (float)u * (1.0f / 8388608.0f);
         break;
       }
-      case MGX_PCM_S32: v = (float)((double)*reinterpret_cast<const int32_t*>(b) * (1.0 / 2147483648.0)); break;
-      default: v = *reinterpret_cast<const float*>(b); break;
+      case MGX_PCM_S32: v = (float)((double)(int32_t)w32() * (1.0 / 2147483648.0)); break;
+      default: v = __builtin_bit_cast(float, w32()); break;
     }
     out[i] = v;
   }

@@ -70,8 +70,15 @@ void bark_scale(int n, double sr, float* out) {
     out[i] = (float)(13 * atan((double)f / 1315.8) + 3.5 * atan(q * q));
   }
 }
-// src/extractors/loudness.js:24-45
+// src/extractors/loudness.js:24-45. len = N/2 is 0 for bufferSize 1 (a power of two the
+// reference accepts): barkScale[-1] is undefined there, so bandEnd is NaN, no limit moves
+// and the last one is length - 1 = -1.
 void bark_limits(const float* bark, int len, int nb, int32_t* lim) {
+  if (len <= 0) {
+    for (int i = 0; i < nb; i++) lim[i] = 0;
+    lim[nb] = len - 1;
+    return;
+  }
   double end = (double)bark[len - 1] / nb;
   int band = 1;
   for (int i = 0; i <= nb; i++) lim[i] = 0;
@@ -597,7 +604,7 @@ int extract_host_chunked(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fi
   return MGX_OK;
 }
 
-uint32_t pcm_bytes(uint32_t format) {
+uint32_t sample_bytes(uint32_t format) {
   switch (format) {
     case MGX_PCM_F32: return 4;
     case MGX_PCM_S16: return 2;
@@ -664,8 +671,8 @@ int mgx_wav_parse(const void* bytes, uint64_t len, mgx_wav_info* info) {
       else if (tag == 3 && bits == 32) fmt = MGX_PCM_F32;
       if (fmt == 0xFFFFFFFFu) return fail(MGX_E_UNSUPPORTED, "unsupported WAV encoding (format tag %u, %u bits)", tag, bits);
       if (channels == 0) return fail(MGX_E_INVALID_ARGUMENT, "WAV with 0 channels");
-      if (align != channels * pcm_bytes(fmt))
-        return fail(MGX_E_INVALID_ARGUMENT, "block_align %u does not match %u channels x %u bytes", align, channels, pcm_bytes(fmt));
+      if (align != channels * sample_bytes(fmt))
+        return fail(MGX_E_INVALID_ARGUMENT, "block_align %u does not match %u channels x %u bytes", align, channels, sample_bytes(fmt));
       const uint64_t avail = len - (off + 8);
       const uint64_t data = std::min<uint64_t>(size, avail);
       info->pcm_format = fmt;
@@ -687,16 +694,16 @@ int mgx_pcm_decode_device(const void* pcm, uint64_t sample_frames, uint32_t form
                           uint32_t channel, float* out, void* stream) {
   if (sample_frames == 0) return MGX_OK;
   if (!pcm || !out) return fail(MGX_E_INVALID_ARGUMENT, "NULL pointer");
-  if (!pcm_bytes(format)) return fail(MGX_E_INVALID_ARGUMENT, "unknown PCM format %u", format);
+  if (!sample_bytes(format)) return fail(MGX_E_INVALID_ARGUMENT, "unknown PCM format %u", format);
   if (channels == 0 || channel >= channels) return fail(MGX_E_INVALID_ARGUMENT, "channel %u of %u", channel, channels);
   hipError_t e = mgx::launch_pcm_decode(pcm, sample_frames, format, channels, channel, out, (hipStream_t)stream);
   return e == hipSuccess ? MGX_OK : hip_fail(e, "PCM decode launch");
 }
 
-int mgx_extract_host_pcm(mgx_plan* p, const void* pcm, uint64_t sample_frames, uint32_t format, uint32_t channels,
-                         uint32_t channel, const mgx_outputs* o) {
+int mgx_extract_host_pcm(mgx_plan* p, const void* pcm, uint64_t pcm_bytes, uint64_t sample_frames, uint32_t format,
+                         uint32_t channels, uint32_t channel, const mgx_outputs* o) {
   if (!p || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL plan or outputs");
-  const uint32_t bps = pcm_bytes(format);
+  const uint32_t bps = sample_bytes(format);
   if (!bps) return fail(MGX_E_INVALID_ARGUMENT, "unknown PCM format %u", format);
   if (channels == 0 || channel >= channels) return fail(MGX_E_INVALID_ARGUMENT, "channel %u of %u", channel, channels);
   if ((o->complex_real == nullptr) != (o->complex_imag == nullptr))
@@ -706,6 +713,9 @@ int mgx_extract_host_pcm(mgx_plan* p, const void* pcm, uint64_t sample_frames, u
   if (nframes == 0) return MGX_OK;
   if (!pcm) return fail(MGX_E_INVALID_ARGUMENT, "pcm is NULL");
   const uint64_t align = (uint64_t)bps * channels;
+  if (sample_frames > pcm_bytes / align)
+    return fail(MGX_E_INVALID_ARGUMENT, "%llu sample frames of %llu bytes exceed the %llu-byte PCM buffer",
+                (unsigned long long)sample_frames, (unsigned long long)align, (unsigned long long)pcm_bytes);
   const uint64_t chunk_bytes = std::min<uint64_t>(nframes, kHostChunk) * n * align;
   if (p->s_pcm_bytes < chunk_bytes) {
     if (p->s_pcm) (void)hipFree(p->s_pcm);

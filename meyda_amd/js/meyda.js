@@ -76,7 +76,8 @@ class Meyda {
     this.hamming = t.hamming;
     this.featureInfo = Object.assign({}, FEATURE_INFO);
     this.signal = null;
-    this._plans = {};
+    this._plans = {};       // streaming / sync plan per window
+    this._asyncPlans = {};  // per window: plans that async batch jobs run on (never the streaming one)
     this._frame = null; // results of the current buffer, filled lazily by get()
     // Web Audio wiring when the context provides it (src/meyda.js:67-94). One node per
     // instance (the reference stored it on a window global).
@@ -90,22 +91,41 @@ class Meyda {
     }
   }
 
-  // One plan per window type, created on first use (windowingFunction may change at
-  // runtime as in the reference, src/meyda.js:41,76,164).
-  _plan() {
+  _window() {
     const w = this.windowingFunction;
     if (w !== 'hanning' && w !== 'hamming') {
       throw new TypeError('unknown windowingFunction "' + w + '"');
     }
-    if (!this._plans[w]) {
-      this._plans[w] = addon.createPlan({
-        bufferSize: this.bufferSize, sampleRate: this.sampleRate, windowingFunction: w,
-        precision: this.options.precision, mode: this.options.mode,
-        numMelBands: this.options.numMelBands, numMfccCoeffs: this.options.numMfccCoeffs,
-        device: this.options.device, scalarF64: 1,
-      });
-    }
+    return w;
+  }
+
+  _newPlan(w) {
+    return addon.createPlan({
+      bufferSize: this.bufferSize, sampleRate: this.sampleRate, windowingFunction: w,
+      precision: this.options.precision, mode: this.options.mode,
+      numMelBands: this.options.numMelBands, numMfccCoeffs: this.options.numMfccCoeffs,
+      device: this.options.device, scalarF64: 1,
+    });
+  }
+
+  // One plan per window type, created on first use (windowingFunction may change at
+  // runtime as in the reference, src/meyda.js:41,76,164). process()/get()/getBatch() run on it.
+  _plan() {
+    const w = this._window();
+    if (!this._plans[w]) this._plans[w] = this._newPlan(w);
     return this._plans[w];
+  }
+
+  // Async batch jobs own their plan for the whole job (the addon marks it busy), so they
+  // never run on the streaming plan: per window, a pool grown on demand, so onaudioprocess
+  // buffers and further async batches proceed while a job is in flight.
+  _asyncPlan() {
+    const w = this._window();
+    const pool = this._asyncPlans[w] || (this._asyncPlans[w] = []);
+    for (const p of pool) if (!addon.planBusy(p)) return p;
+    const p = this._newPlan(w);
+    pool.push(p);
+    return p;
   }
 
   // The per-buffer handler (src/meyda.js:69-91): take the buffer, then deliver the
@@ -238,7 +258,7 @@ class Meyda {
 
   getBatchAsync(features, frames) {
     const names = checkBatchNames(features);
-    return addon.extractAsync(this._plan(), toF32(frames), names);
+    return addon.extractAsync(this._asyncPlan(), toF32(frames), names);
   }
 
   // Every full buffer of a .wav file (Buffer / Uint8Array / ArrayBuffer), channel `channel`.
@@ -247,7 +267,7 @@ class Meyda {
   }
 
   getBatchWavAsync(features, wavBytes, channel) {
-    return addon.extractWavAsync(this._plan(), wavBytes, checkBatchNames(features), channel | 0);
+    return addon.extractWavAsync(this._asyncPlan(), wavBytes, checkBatchNames(features), channel | 0);
   }
 
   static readWav(wavBytes) {
@@ -259,9 +279,14 @@ class Meyda {
     return frameValue(name, result, index, bufferSize, numMfccCoeffs);
   }
 
+  // Frees the device plans now. A plan an async job still owns is left to that job: the
+  // addon keeps it alive until the job settles and the GC then frees it.
   dispose() {
-    for (const k of Object.keys(this._plans)) addon.destroyPlan(this._plans[k]);
+    const all = Object.values(this._plans);
+    for (const pool of Object.values(this._asyncPlans)) all.push(...pool);
+    for (const p of all) if (!addon.planBusy(p)) addon.destroyPlan(p);
     this._plans = {};
+    this._asyncPlans = {};
   }
 }
 

@@ -94,4 +94,14 @@ check('readWav (RIFF walk in the library, no device)', () => {
   assert.throws(() => Meyda.readWav(Buffer.from('not a wav file at all')), /RIFF/);
 });
 
+check('bufferSize 1 and 2 construct (isPowerOfTwo accepts them; tables only)', () => {
+  for (const N of [1, 2]) {
+    const m = new Meyda(ctx, null, N);
+    assert.strictEqual(m.hanning.length, N);
+    assert.strictEqual(m.barkScale.length, N);
+  }
+  const t = Meyda.addon.hostTables({ bufferSize: 1 });
+  assert.strictEqual(t.barkLimits[24], -1);  // loudness.js:44: normalisedSpectrum.length - 1
+});
+
 console.log('facade_cpu: ' + n + ' checks passed');

@@ -163,6 +163,42 @@ check('literal (snapshot) mode is bit-exact', () => {
   m.dispose();
 });
 
+check('async batch jobs run on their own plan: streaming continues meanwhile', () => {
+  const seen = [];
+  const m = new Meyda(ctx, null, 512, (feat) => seen.push(feat));
+  m.start(['rms', 'zcr']);
+  const F = 64;
+  const x = g.input.subarray(0, F * 512);
+  const p1 = m.getBatchAsync(['rms', 'mfcc'], x);
+  const p2 = m.getBatchAsync(['zcr'], x);       // a second job while the first is pending
+  for (let i = 0; i < 6; i++) m.process(frameOf(g, i));   // onaudioprocess during the jobs
+  assert.strictEqual(seen.length, 6);
+  for (let i = 0; i < 6; i++) assert.strictEqual(seen[i].zcr, g.scalars[i * S + 2]);
+  m.dispose();                                  // busy plans are left to their jobs
+  return Promise.all([p1, p2]).then(([a, b]) => {
+    assert.strictEqual(a.rms.length, F);
+    for (let i = 0; i < F; i++) assert.strictEqual(b.zcr[i], g.scalars[i * S + 2]);
+  });
+});
+
+check('plan handle collected while an async job runs (no use-after-free)', () => {
+  assert.ok(typeof global.gc === 'function', 'run node with --expose-gc');
+  const x = g.input.subarray(0, 90 * 512);
+  const jobs = [];
+  for (let k = 0; k < 4; k++) {
+    // the Meyda instance (and its plans) become unreachable right away
+    jobs.push(new Meyda(ctx, null, 512).getBatchAsync(['rms', 'spectralCentroid', 'mfcc'], x));
+  }
+  global.gc();
+  return Promise.all(jobs).then((rs) => {
+    global.gc();
+    for (const r of rs) {
+      assert.strictEqual(r.rms.length, 90);
+      for (let i = 0; i < 90; i += 11) close(r.rms[i], g.scalars[i * S + 0], 1e-5, 0, 'rms');
+    }
+  });
+});
+
 (async () => {
   for (const [name, fn] of checks) {
     await fn();

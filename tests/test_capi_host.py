@@ -36,7 +36,7 @@ def test_exports_every_header_symbol(capi):
 
 def test_abi_version_and_names(capi):
     L = capi.lib()
-    assert L.mgx_abi_version() == 1
+    assert L.mgx_abi_version() == 2
     for i, name in enumerate(capi.FEATURE_NAMES):
         assert L.mgx_feature_name(i).decode() == name
         assert L.mgx_feature_index(name.encode()) == i
@@ -99,3 +99,16 @@ def test_no_silent_cpu_fallback(capi):
     with pytest.raises(capi.MgxError) as ei:
         capi.Plan(buffer_size=1024)
     assert ei.value.status == -6
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_host_tables_tiny_buffer_sizes(capi, n):
+    # isPowerOfTwo accepts 1 (src/utils.js:13-19), so new Meyda(ctx, src, 1) builds tables:
+    # N/2 = 0 bins leaves barkScale[-1] undefined in computeBarkBandLimits
+    # (loudness.js:24-45): no limit moves and the last is length - 1 = -1.
+    t = capi.host_tables(buffer_size=n)
+    L = n // 2
+    assert t["bark_limits"][-1] == L - 1
+    if L == 0:
+        assert np.all(t["bark_limits"][:-1] == 0)
+    assert t["hanning"].shape == (n,) and t["bark_scale"].shape == (n,)

@@ -14,7 +14,7 @@ def run_node(script):
         pytest.skip("node is not installed")
     if not os.path.exists(ADDON):
         pytest.skip("N-API addon not built (make -C meyda_amd/addon)")
-    r = subprocess.run(["node", os.path.join(ROOT, "tests", "js", script)], capture_output=True, text=True,
+    r = subprocess.run(["node", "--expose-gc", os.path.join(ROOT, "tests", "js", script)], capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return r.stdout
@@ -22,10 +22,10 @@ def run_node(script):
 
 def test_facade_host_side():
     out = run_node("facade_cpu.js")
-    assert "facade_cpu: 7 checks passed" in out
+    assert "facade_cpu: 8 checks passed" in out
 
 
 @pytest.mark.gpu
 def test_facade_on_gpu():
     out = run_node("facade_gpu.js")
-    assert "facade_gpu: 8 checks passed" in out
+    assert "facade_gpu: 10 checks passed" in out

@@ -126,3 +126,33 @@ def test_wav_of_reference_frames_matches_reference_features(capi):
     assert not tolerance.check_vectors(out["mfcc"], g["mfcc"][idx])
     rms = out["rms"]
     assert np.allclose(rms, g["scalars"][idx, 0], rtol=1e-5, atol=0)
+
+
+@pytest.mark.gpu
+def test_extract_pcm_rejects_short_buffer_and_decodes_unaligned(capi):
+    import torch
+    n = 512
+    rng = np.random.default_rng(5)
+    codes = wavgen.random_codes(rng, 4 * n, 1, "s16")
+    raw = wavgen.wav_bytes(codes, "s16")
+    info = capi.wav_parse(raw)
+    pcm = np.frombuffer(raw, np.uint8)[info["data_offset"]:info["data_offset"] + info["data_bytes"]]
+    plan = capi.Plan(buffer_size=n)
+    # claiming more sample frames than the buffer holds is refused before any copy
+    with pytest.raises(capi.MgxError) as ei:
+        plan.extract_pcm(pcm[:-2], 4 * n, "s16", 1, 0, ["rms"])
+    assert ei.value.status == -1
+    # device decode from an odd byte address (a caller's pointer need not be aligned)
+    for fmt in ("s16", "s32", "f32"):
+        c = wavgen.random_codes(rng, 777, 1, fmt)
+        body = np.frombuffer(wavgen.wav_bytes(c, fmt), np.uint8)
+        inf = capi.wav_parse(body.tobytes())
+        data = body[inf["data_offset"]:inf["data_offset"] + inf["data_bytes"]]
+        dev = torch.zeros(data.size + 1, dtype=torch.uint8, device="cuda")
+        dev[1:] = torch.from_numpy(data.copy()).cuda()
+        out = torch.empty(777, dtype=torch.float32, device="cuda")
+        check = capi.lib().mgx_pcm_decode_device(dev.data_ptr() + 1, 777, capi.PCM_FORMATS[fmt], 1, 0,
+                                                 out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        assert check == 0
+        want = wavgen.decode(c[:, 0], fmt)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32)), fmt
