@@ -6,13 +6,13 @@ ARCH ?= gfx950
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Wno-unused-result \
            -mllvm -disable-machine-licm
 LIB = meyda_amd/libmeyda_gpu.so
-SRC = meyda_amd/csrc/kernels.hip meyda_amd/csrc/plan.cpp
+SRC = meyda_amd/csrc/kernels.hip meyda_amd/csrc/plan.cpp meyda_amd/csrc/group.cpp
 HDR = include/meyda_gpu.h meyda_amd/csrc/mgx_internal.h
 
 all: $(LIB) oracle
 
 $(LIB): $(SRC) $(HDR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ -x hip $(SRC)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ -x hip $(SRC) -ldl
 
 oracle:
 	$(MAKE) -s -C oracle

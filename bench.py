@@ -8,10 +8,17 @@ A "step" is one fused extraction launch over one batch of 262,144 synthetic fram
 of 1024 float32 samples per GPU (BASELINE config C3/C4 size), computing every
 per-frame feature: rms, energy, zcr, spectralCentroid/Flatness/Slope/Rolloff/
 Spread/Skewness/Kurtosis, loudness (24 specific + total), perceptualSpread,
-perceptualSharpness, mfcc (13). Inputs are generated in HBM before the timed
-region. Multi-GPU: one process per GPU (torch.distributed), each rank extracts
-its own 262,144-frame shard (weak scaling, no data-path collective); rank 0
-prints the JSON line with the whole-job frames/s (max elapsed over ranks).
+perceptualSharpness, mfcc (13 coefficients of the reference's 26 mel bands).
+Inputs are generated in HBM before the timed region.
+
+Multi-GPU (torchrun, one process per GPU): each rank extracts its own 262,144-frame
+shard of one global stream (weak scaling) through the library's multi-device group
+(include/meyda_gpu.h, mgx_group_create_rank), which gathers every rank's per-frame
+feature records to rank 0 over xGMI with RCCL point-to-point transfers, chunked so
+that chunk i's transfer overlaps chunk i+1's extraction (the north star's gather is
+inside the timed step; --no-gather times the shards alone). torch.distributed (gloo)
+is only the control plane: the RCCL id broadcast, barriers and the max-over-ranks
+elapsed time. Rank 0 prints the JSON line with the whole-job frames/s.
 """
 import argparse
 import concurrent.futures as cf
@@ -47,8 +54,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--also-fast", action="store_true", help="report the fp32 mode alongside")
-    ap.add_argument("--gather", action="store_true",
-                    help="gather every rank's feature record to rank 0 inside the timed step (RCCL)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: time the shards alone, without the RCCL gather to rank 0")
+    ap.add_argument("--chunks", type=int, default=0, help="N > 1: gather pipeline depth (0 = automatic)")
     return ap.parse_args()
 
 
@@ -84,22 +92,28 @@ def capi_seed():
     return meyda_amd.SEED
 
 
-def settle(plan, frames, out, ms):
-    """Untimed launches for `ms` of wall time (clock ramp-up), before the warmup steps."""
+def settle(step, ms, dist=None):
+    """Untimed steps for `ms` of wall time (clock ramp-up), before the warmup steps."""
     stream = torch.cuda.current_stream()
     t0 = time.perf_counter()
-    while (time.perf_counter() - t0) * 1e3 < ms:
+    go = True
+    while go:
         for _ in range(8):
-            plan.extract_device(frames.data_ptr(), frames.shape[0], out, stream.cuda_stream)
+            step(stream.cuda_stream)
         torch.cuda.synchronize()
+        go = (time.perf_counter() - t0) * 1e3 < ms
+        if dist:  # every rank runs the same number of (collective) steps
+            t = torch.tensor([1 if go else 0], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            go = bool(t.item())
 
 
-def run_mode(plan, frames, out, steps, warmup, dist, world, gather=None):
+def run_mode(step, steps, warmup, dist):
+    """W untimed steps, then exactly `steps` timed ones bracketed by a barrier and a device
+    synchronisation on both sides; HIP events on the launch stream around each step."""
     stream = torch.cuda.current_stream()
     for _ in range(warmup):
-        plan.extract_device(frames.data_ptr(), frames.shape[0], out, stream.cuda_stream)
-        if gather:
-            gather()
+        step(stream.cuda_stream)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -108,17 +122,15 @@ def run_mode(plan, frames, out, steps, warmup, dist, world, gather=None):
     t0 = time.perf_counter()
     for i in range(steps):
         ev[i][0].record(stream)
-        plan.extract_device(frames.data_ptr(), frames.shape[0], out, stream.cuda_stream)
+        step(stream.cuda_stream)
         ev[i][1].record(stream)
-        if gather:
-            gather()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if dist:
-        t = torch.tensor([elapsed], device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, kernel_ms
@@ -129,30 +141,46 @@ def main():
     from meyda_amd import dist as mdist
     rank, local, world = mdist.env_rank_world()
     dist = None
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as tdist
-        mdist.init("nccl")
+        mdist.init("gloo")  # control plane only; the data path is the library's RCCL gather
         dist = tdist
-    else:
-        torch.cuda.set_device(0)
     n, F = args.n, args.frames
     frames = torch.empty(F, n, dtype=torch.float32, device="cuda")
     # each rank its own shard of one global synthetic stream
     capi.synth_frames_device(frames, capi_seed(), first_frame=rank * F)
-    plan = capi.Plan(buffer_size=n, precision=args.precision, device=torch.cuda.current_device())
-    outs, o = plan.alloc_outputs(F, FEATURES)
+    dev = torch.cuda.current_device()
+    plan = capi.Plan(buffer_size=n, precision=args.precision, device=dev)
+    gather = world > 1 and not args.no_gather
+    if gather:
+        uid = [capi.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        group = capi.Group(buffer_size=n, rank=rank, nranks=world, unique_id=uid[0], precision=args.precision,
+                           device=dev)
+        # rank 0 holds the whole job's feature record; the other ranks only their transfer buffers
+        outs, o = plan.alloc_outputs(F * world if rank == 0 else 1, FEATURES)
+        mask = capi.output_mask(o)
+        root = o if rank == 0 else None
+
+        def step(s):
+            group.extract_device([frames.data_ptr()], [F] * world, root, mask, args.chunks, [s])
+    else:
+        outs, o = plan.alloc_outputs(F, FEATURES)
+
+        def step(s):
+            plan.extract_device(frames.data_ptr(), F, o, s)
     torch.cuda.synchronize()
-    gather = None
-    if args.gather and dist:
-        counts = [F] * world
-        gather = lambda: mdist.gather_features(outs, counts, dst=0)  # noqa: E731
-    settle(plan, frames, o, args.settle_ms)
-    elapsed, kernel_ms = run_mode(plan, frames, o, args.steps, args.warmup, dist, world, gather)
+    settle(step, args.settle_ms, dist)
+    elapsed, kernel_ms = run_mode(step, args.steps, args.warmup, dist)
     fast = None
-    if args.also_fast and args.precision != "fast":
-        plan_f = capi.Plan(buffer_size=n, precision="fast", device=torch.cuda.current_device())
-        settle(plan_f, frames, o, args.settle_ms)
-        el_f, km_f = run_mode(plan_f, frames, o, args.steps, args.warmup, dist, world)
+    if args.also_fast and args.precision != "fast" and world == 1:
+        plan_f = capi.Plan(buffer_size=n, precision="fast", device=dev)
+
+        def step_f(s):
+            plan_f.extract_device(frames.data_ptr(), F, o, s)
+        settle(step_f, args.settle_ms)
+        el_f, km_f = run_mode(step_f, args.steps, args.warmup, dist)
         fast = {"value": world * F * args.steps / el_f, "kernel_ms": km_f,
                 "roofline_frac": (F * (4 * n + 4 * OUT_FLOATS)) / (km_f * 1e-3) / 1e9 / HBM_PEAK_GBS}
     if rank == 0:
@@ -193,8 +221,11 @@ def main():
             "data": "synthetic (seeded splitmix64 PCM generated in HBM)",
             "config": {"workload": "C3+C4 all features: %d frames x bufferSize=%d per GPU, float32 outputs" % (F, n),
                        "buffer_size": n, "frames_per_gpu": F, "features": FEATURES,
+                       "mel_bands": 26, "mfcc_coeffs": 13,
                        "precision": args.precision, "parallelism": "frame shards, %d proc" % world,
-                       "gather_to_rank0": bool(gather)},
+                       "gather_to_rank0": bool(gather),
+                       "gather": ("RCCL send/recv to rank 0 in the timed step, %s chunks" % (args.chunks or "auto"))
+                       if gather else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,

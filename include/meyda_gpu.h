@@ -21,6 +21,9 @@
  *   mgx_wav_parse,       decodeAudioData + getChannelData(0)        lib/bufferLoader.js:23,
  *   mgx_pcm_decode_device,                                          src/meyda.js:72
  *   mgx_extract_host_pcm
+ *   mgx_group_*          several devices, RCCL gather of the        src/meyda.js:17-97 (one plan
+ *                        per-frame records to the root device       per device), :69-91 (buffers
+ *                                                                   are independent: shardable)
  *   mgx_feature_index    the extractor registry by name             src/extractors/index.js:1-20
  *   mgx_feature_info     featureInfo[name].type                     src/feature-info.js:1-65
  *   mgx_last_error       console.error / thrown Error text          src/meyda.js:20-26,249-253
@@ -205,6 +208,71 @@ int mgx_pcm_decode_device(const void* pcm, uint64_t sample_frames, uint32_t form
  * (no read past the caller's buffer). `pcm` needs no alignment. */
 int mgx_extract_host_pcm(mgx_plan* plan, const void* pcm, uint64_t pcm_bytes, uint64_t sample_frames,
                          uint32_t format, uint32_t channels, uint32_t channel, const mgx_outputs* outputs);
+
+/* ---- Multi-device groups -------------------------------
+ * Replaces nothing in the reference (single-threaded browser code); it exists because
+ * buffers are independent (src/meyda.js:69-91 keeps no cross-buffer state), so a batch
+ * is cut into contiguous shards, one per device, each extracted by that device's plan
+ * (the plan of `new Meyda(...)`, src/meyda.js:17-97), and the per-frame feature records
+ * are gathered to the root device (rank 0) over xGMI by RCCL point-to-point transfers.
+ * The gather is chunked: chunk i of every shard is sent while chunk i+1 is extracted.
+ * RCCL (librccl.so.1, or $MGX_RCCL_LIB) is loaded when a group of more than one rank is
+ * created; a one-rank group needs no RCCL. */
+typedef struct mgx_group mgx_group;
+
+#define MGX_COMM_ID_BYTES 128  /* an RCCL unique id (ncclUniqueId) */
+
+/* Output selection of a group extraction (every rank passes the same mask). */
+#define MGX_OUT_SCALAR(i) (1u << (i))       /* i < MGX_NUM_SCALARS */
+#define MGX_OUT_LOUDNESS_SPECIFIC (1u << 13)
+#define MGX_OUT_MFCC (1u << 14)
+#define MGX_OUT_AMPLITUDE_SPECTRUM (1u << 15)
+#define MGX_OUT_POWER_SPECTRUM (1u << 16)
+#define MGX_OUT_COMPLEX_SPECTRUM (1u << 17)   /* real and imag */
+#define MGX_OUT_ALL_MASK ((1u << 18) - 1)
+
+/* Contiguous shard [*start, *start + *count) of `total` frames for `rank` of `nranks`:
+ * the first total % nranks ranks get one frame more. Host only. */
+int mgx_shard_range(uint64_t total, uint32_t nranks, uint32_t rank, uint64_t* start, uint64_t* count);
+
+/* Byte offsets of the outputs of `num_frames` frames packed into one transfer buffer
+ * (structure of arrays, each array 256-byte aligned, in mgx_outputs order: 13 scalars,
+ * loudness_specific, mfcc, amplitude, power, complex real, complex imag). offsets[i] is
+ * the offset of field i (MGX_OUT_* bit i; the complex field has two arrays: offsets[17]
+ * real, offsets[18] imag), or UINT64_MAX when not in `mask`. Returns the total bytes.
+ * Host only; the root unpacks each peer's chunk with the same arithmetic. */
+uint64_t mgx_packed_layout(const mgx_plan_desc* desc, uint32_t mask, uint64_t num_frames, uint64_t offsets[19]);
+
+/* Single process, several devices (RCCL ncclCommInitAll): devices[0] is the root. */
+int mgx_group_create(const mgx_plan_desc* desc, const int32_t* devices, uint32_t num_devices, mgx_group** out);
+
+/* One process per device (e.g. torchrun): rank 0 calls mgx_comm_unique_id and the caller
+ * broadcasts the bytes; every rank then calls mgx_group_create_rank with its rank.
+ * desc->device is this rank's device. Rank 0 is the root. */
+int mgx_comm_unique_id(void* id, uint64_t id_bytes);
+int mgx_group_create_rank(const mgx_plan_desc* desc, const void* unique_id, uint32_t nranks, uint32_t rank,
+                          mgx_group** out);
+int mgx_group_destroy(mgx_group* group);
+/* Ranks of the group, and the ranks this process drives (num_local = 1 per process, or
+ * all of them in single-process mode, first_local = their first rank). */
+int mgx_group_info(const mgx_group* group, uint32_t* nranks, uint32_t* first_local, uint32_t* num_local);
+
+/* Device-resident batch. frames[i]: device pointer of the shard of local rank
+ * first_local + i (on that rank's device); counts: frames of every rank (nranks
+ * entries, the same on every rank; shard r holds global frames [sum counts[<r],
+ * + counts[r])). root_out: device pointers on the root device sized for sum(counts)
+ * frames (read on the root only; may be NULL elsewhere); every field in `mask` must be
+ * non-NULL there. num_chunks: pipeline depth (0 = automatic). streams[i] (or NULL):
+ * the work is ordered after what is enqueued on local rank i's stream, and that stream
+ * waits for its completion (gather included). Asynchronous. */
+int mgx_group_extract_device(mgx_group* group, const float* const* frames, const uint64_t* counts,
+                             const mgx_outputs* root_out, uint32_t mask, uint32_t num_chunks,
+                             void* const* streams);
+
+/* Host batch in, host outputs (single-process groups): the frames are cut into one
+ * shard per device (mgx_shard_range), copied to the devices in parallel, extracted,
+ * gathered to the root device by RCCL and copied back. Output layout as mgx_extract_host. */
+int mgx_group_extract_host(mgx_group* group, const float* frames, uint64_t num_frames, const mgx_outputs* outputs);
 
 int mgx_is_power_of_two(double n);           /* src/utils.js:13-19 */
 int mgx_feature_index(const char* name);     /* -1 if unknown */

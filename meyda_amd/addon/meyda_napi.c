@@ -4,7 +4,10 @@
  * allocation and error translation; all compute is in libmeyda_gpu.so.
  *
  * Exports:
- *   createPlan(opts)                     -> plan handle (external; destroyed by GC or destroyPlan)
+ *   createPlan(opts)                     -> plan handle (external; destroyed by GC or destroyPlan);
+ *                                           opts.devices = [d0, d1, ...] makes a multi-device
+ *                                           plan: batches are sharded over the devices and the
+ *                                           features gathered to d0 by RCCL (mgx_group_*)
  *   destroyPlan(plan)
  *   planBusy(plan)                       -> true while an async extraction owns the plan
  *   extract(plan, frames, features)      -> { name: TypedArray }   (synchronous)
@@ -43,6 +46,7 @@ static napi_value throw_mgx(napi_env env, int rc) {
 
 typedef struct {
   mgx_plan* plan;
+  mgx_group* group;  /* createPlan({devices: [...]}): a multi-device group */
   mgx_plan_desc desc;
   int busy;       /* an async extraction owns the plan */
   int finalized;  /* the JS handle was collected while busy: async_complete frees the box */
@@ -50,6 +54,7 @@ typedef struct {
 
 static void plan_box_free(plan_box* b) {
   if (b->plan) mgx_plan_destroy(b->plan);
+  if (b->group) mgx_group_destroy(b->group);
   free(b);
 }
 
@@ -105,7 +110,7 @@ static int get_str_prop(napi_env env, napi_value obj, const char* name, char* bu
 }
 
 /* opts: { bufferSize, sampleRate, windowingFunction, precision, mode, numMelBands,
- *         numMfccCoeffs, device, scalarF64 } */
+ *         numMfccCoeffs, device, scalarF64, devices } */
 static int desc_from_opts(napi_env env, napi_value opts, mgx_plan_desc* d) {
   mgx_plan_desc_init(d);
   d->scalar_f64 = 1;
@@ -141,11 +146,41 @@ static napi_value create_plan(napi_env env, napi_callback_info info) {
   }
   mgx_plan_desc d;
   desc_from_opts(env, argv[0], &d);
+  /* devices: [d0, d1, ...] shards every batch over those devices (d0 is the root) */
+  int32_t devs[64];
+  uint32_t ndev = 0;
+  bool has = false, is_arr = false;
+  napi_has_named_property(env, argv[0], "devices", &has);
+  if (has) {
+    napi_value arr;
+    CHECK(napi_get_named_property(env, argv[0], "devices", &arr));
+    napi_is_array(env, arr, &is_arr);
+    if (is_arr) {
+      napi_get_array_length(env, arr, &ndev);
+      if (ndev == 0 || ndev > 64) {
+        napi_throw_range_error(env, NULL, "devices must list 1 to 64 device ordinals");
+        return NULL;
+      }
+      for (uint32_t i = 0; i < ndev; ++i) {
+        napi_value v;
+        int32_t dv = -1;
+        napi_get_element(env, arr, i, &v);
+        if (napi_get_value_int32(env, v, &dv) != napi_ok) {
+          napi_throw_type_error(env, NULL, "devices must be numbers");
+          return NULL;
+        }
+        devs[i] = dv;
+      }
+      d.device = devs[0];
+    }
+  }
   mgx_plan* p = NULL;
-  int rc = mgx_plan_create(&d, &p);
+  mgx_group* grp = NULL;
+  int rc = ndev > 0 ? mgx_group_create(&d, devs, ndev, &grp) : mgx_plan_create(&d, &p);
   if (rc) return throw_mgx(env, rc);
   plan_box* b = (plan_box*)calloc(1, sizeof *b);
   b->plan = p;
+  b->group = grp;
   b->desc = d;
   napi_value ext;
   CHECK(napi_create_external(env, b, plan_finalize, NULL, &ext));
@@ -159,7 +194,7 @@ static plan_box* get_plan(napi_env env, napi_value v) {
     return NULL;
   }
   plan_box* b = (plan_box*)data;
-  if (!b->plan) {
+  if (!b->plan && !b->group) {
     napi_throw_error(env, NULL, "plan was destroyed");
     return NULL;
   }
@@ -186,8 +221,10 @@ static napi_value destroy_plan(napi_env env, napi_callback_info info) {
     napi_throw_error(env, NULL, "plan is busy with an async extraction");
     return NULL;
   }
-  mgx_plan_destroy(b->plan);
+  if (b->plan) mgx_plan_destroy(b->plan);
+  if (b->group) mgx_group_destroy(b->group);
   b->plan = NULL;
+  b->group = NULL;
   return NULL;
 }
 
@@ -380,7 +417,14 @@ static int job_prepare_wav(napi_env env, job* j, napi_value wav_v, napi_value fe
 }
 
 static void job_run(job* j) {
-  if (j->pcm)
+  if (j->box->group && j->pcm) {
+    j->rc = MGX_E_UNSUPPORTED;
+    snprintf(j->err, sizeof j->err, "extractWav on a multi-device plan: use a single-device plan");
+    return;
+  }
+  if (j->box->group)
+    j->rc = mgx_group_extract_host(j->box->group, j->frames, j->nframes, &j->out);
+  else if (j->pcm)
     j->rc = mgx_extract_host_pcm(j->box->plan, j->pcm, j->pcm_bytes, j->pcm_frames, j->pcm_format, j->pcm_channels,
                                  j->pcm_channel, &j->out);
   else

@@ -33,7 +33,17 @@ EXPORTS = ["mgx_plan_desc_init", "mgx_plan_create", "mgx_plan_destroy", "mgx_pla
            "mgx_extract_device", "mgx_extract_host", "mgx_synth_frames_device",
            "mgx_get_host_tables", "mgx_is_power_of_two", "mgx_feature_index", "mgx_feature_name",
            "mgx_feature_info", "mgx_device_count", "mgx_abi_version", "mgx_last_error",
-           "mgx_wav_parse", "mgx_pcm_decode_device", "mgx_extract_host_pcm"]
+           "mgx_wav_parse", "mgx_pcm_decode_device", "mgx_extract_host_pcm",
+           "mgx_shard_range", "mgx_packed_layout", "mgx_comm_unique_id", "mgx_group_create",
+           "mgx_group_create_rank", "mgx_group_destroy", "mgx_group_info", "mgx_group_extract_device",
+           "mgx_group_extract_host"]
+COMM_ID_BYTES = 128
+# output selection bits of a group extraction (MGX_OUT_* in include/meyda_gpu.h)
+OUT_LOUDNESS_SPECIFIC, OUT_MFCC, OUT_AMPLITUDE, OUT_POWER, OUT_COMPLEX = (1 << 13, 1 << 14, 1 << 15, 1 << 16,
+                                                                          1 << 17)
+# field order of mgx_packed_layout / mgx_outputs
+FIELDS = SCALAR_NAMES + ["loudness.specific", "mfcc", "amplitudeSpectrum", "powerSpectrum",
+                         "complexSpectrum.real", "complexSpectrum.imag"]
 PCM_FORMATS = {"f32": 0, "s16": 1, "u8": 2, "s24": 3, "s32": 4}
 
 
@@ -88,6 +98,11 @@ def lib():
         # two HIP runtimes in one process leave the second without devices.
         try:
             import torch  # noqa: F401
+            # multi-device groups load RCCL at run time: in a torch process use torch's own
+            # librccl (built against the HIP runtime this process runs on)
+            trccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+            if "MGX_RCCL_LIB" not in os.environ and os.path.exists(trccl):
+                os.environ["MGX_RCCL_LIB"] = trccl
         except ImportError:
             pass
         L = ctypes.CDLL(LIB_PATH)
@@ -115,6 +130,23 @@ def lib():
                                             ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         L.mgx_extract_host_pcm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(Outputs)]
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.mgx_shard_range.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, u64p, u64p]
+        L.mgx_packed_layout.argtypes = [ctypes.POINTER(PlanDesc), ctypes.c_uint32, ctypes.c_uint64, u64p]
+        L.mgx_packed_layout.restype = ctypes.c_uint64
+        L.mgx_comm_unique_id.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.mgx_group_create.argtypes = [ctypes.POINTER(PlanDesc), ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32,
+                                       ctypes.POINTER(ctypes.c_void_p)]
+        L.mgx_group_create_rank.argtypes = [ctypes.POINTER(PlanDesc), ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
+        L.mgx_group_destroy.argtypes = [ctypes.c_void_p]
+        L.mgx_group_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                     ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+        L.mgx_group_extract_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), u64p,
+                                               ctypes.POINTER(Outputs), ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.POINTER(ctypes.c_void_p)]
+        L.mgx_group_extract_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.POINTER(Outputs)]
         _lib = L
     return _lib
 
@@ -296,6 +328,93 @@ class Plan:
 
 
 ALL_FEATURES = SCALAR_NAMES[:10] + ["loudness", "perceptualSpread", "perceptualSharpness", "mfcc"]
+
+
+def shard_range(total, nranks, rank):
+    """(start, count) of rank's contiguous shard (mgx_shard_range; host only)."""
+    s, c = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().mgx_shard_range(total, nranks, rank, ctypes.byref(s), ctypes.byref(c)))
+    return s.value, c.value
+
+
+def output_mask(outputs):
+    """MGX_OUT_* mask of the non-NULL fields of an Outputs structure."""
+    m = 0
+    for i in range(NUM_SCALARS):
+        if outputs.scalars[i]:
+            m |= 1 << i
+    for bit, f in ((13, "loudness_specific"), (14, "mfcc"), (15, "amplitude_spectrum"),
+                   (16, "power_spectrum"), (17, "complex_real")):
+        if getattr(outputs, f):
+            m |= 1 << bit
+    return m
+
+
+def packed_layout(desc, mask, num_frames):
+    """(total_bytes, {field: offset}) of mgx_packed_layout (host only)."""
+    off = (ctypes.c_uint64 * 19)()
+    total = lib().mgx_packed_layout(ctypes.byref(desc), mask, num_frames, off)
+    return total, {FIELDS[i]: off[i] for i in range(19) if off[i] != 2 ** 64 - 1}
+
+
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    check(lib().mgx_comm_unique_id(buf, COMM_ID_BYTES))
+    return buf.raw
+
+
+class Group:
+    """Frames sharded over several devices with an RCCL gather of the feature records to the
+    root (rank 0) — include/meyda_gpu.h "Multi-device groups".
+
+    Group(devices=[0, 1, ...], **plan_kw)                 one process, several devices
+    Group(rank=r, nranks=n, unique_id=b, device=d, ...)   one process per device (torchrun)
+    """
+
+    def __init__(self, buffer_size=512, devices=None, rank=None, nranks=None, unique_id=None, **kw):
+        h = ctypes.c_void_p()
+        if devices is not None:
+            self.desc = make_desc(buffer_size=buffer_size, device=devices[0], **kw)
+            arr = (ctypes.c_int32 * len(devices))(*devices)
+            check(lib().mgx_group_create(ctypes.byref(self.desc), arr, len(devices), ctypes.byref(h)))
+        else:
+            self.desc = make_desc(buffer_size=buffer_size, **kw)
+            check(lib().mgx_group_create_rank(ctypes.byref(self.desc), unique_id, nranks, rank, ctypes.byref(h)))
+        self._h = h
+        self.n = buffer_size
+        self.scalar_dtype = np.float64 if kw.get("scalar_f64") else np.float32
+        nr, first, nl = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().mgx_group_info(h, ctypes.byref(nr), ctypes.byref(first), ctypes.byref(nl)))
+        self.nranks, self.first_local, self.num_local = nr.value, first.value, nl.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mgx_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def extract_device(self, frames_ptrs, counts, root_outputs, mask, num_chunks=0, streams=None):
+        """frames_ptrs: device pointers of the local ranks' shards; counts: frames of every
+        rank; root_outputs: an Outputs of device pointers on the root (None elsewhere)."""
+        fp = (ctypes.c_void_p * len(frames_ptrs))(*frames_ptrs)
+        cn = (ctypes.c_uint64 * len(counts))(*counts)
+        st = None if streams is None else (ctypes.c_void_p * len(streams))(*streams)
+        check(lib().mgx_group_extract_device(self._h, fp, cn, None if root_outputs is None else ctypes.byref(root_outputs),
+                                             mask, num_chunks, st))
+
+    def extract(self, frames, features):
+        """Host numpy in / numpy out, sharded over the group's devices (single process)."""
+        frames = np.ascontiguousarray(frames, dtype=np.float32)
+        F, n = frames.shape
+        assert n == self.n
+        out, o = Plan._host_outputs(self, F, features)
+        check(lib().mgx_group_extract_host(self._h, frames.ctypes.data, F, ctypes.byref(o)))
+        return out
 
 
 def synth_frames_device(tensor, seed, first_frame=0, stream=None):

@@ -1,0 +1,540 @@
+// Multi-device groups (include/meyda_gpu.h, "Multi-device groups").
+//
+// Buffers are independent in the reference (src/meyda.js:69-91 keeps no state from one
+// buffer to the next), so a batch is cut into contiguous shards, one per device. Each
+// device runs its own plan (src/meyda.js:17-97: the tables of `new Meyda(...)`) on its
+// shard, chunk by chunk. A non-root rank extracts chunk c straight into one packed
+// transfer buffer (structure of arrays) and sends it to the root with ncclSend on its
+// communication stream while chunk c+1 is extracted on the compute stream (two buffers
+// alternate); the root extracts its own shard straight into its outputs, receives every
+// peer's chunk into a staging slot (ncclRecv) and scatters it into place with one small
+// kernel on the communication stream. RCCL is loaded at run time (dlopen), so the library
+// has no link-time dependency on it and a one-rank group never touches it.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mgx_internal.h"
+
+using mgx::fail;
+using mgx::hip_fail;
+
+namespace {
+
+// ------------------------------------------------------------------ RCCL loader
+struct Rccl {
+  bool ok = false;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+// Loaded once per process: $MGX_RCCL_LIB, else librccl.so.1 from the loader path, else
+// the ROCm installation's copy.
+Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (tried) return r.ok ? &r : nullptr;
+  tried = true;
+  void* h = nullptr;
+  const char* env = getenv("MGX_RCCL_LIB");
+  const char* names[] = {env, "librccl.so.1", "/opt/rocm/lib/librccl.so.1"};
+  for (const char* n : names)
+    if (n && (h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+  if (!h) return nullptr;
+  bool all = true;
+  auto sym = [&](auto& fn, const char* name) {
+    fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+    all = all && fn != nullptr;
+  };
+  sym(r.GetUniqueId, "ncclGetUniqueId");
+  sym(r.CommInitRank, "ncclCommInitRank");
+  sym(r.CommInitAll, "ncclCommInitAll");
+  sym(r.CommDestroy, "ncclCommDestroy");
+  sym(r.GroupStart, "ncclGroupStart");
+  sym(r.GroupEnd, "ncclGroupEnd");
+  sym(r.Send, "ncclSend");
+  sym(r.Recv, "ncclRecv");
+  sym(r.GetErrorString, "ncclGetErrorString");
+  r.ok = all;
+  return r.ok ? &r : nullptr;
+}
+
+int rccl_fail(ncclResult_t e, const char* what) {
+  Rccl* r = rccl();
+  return fail(MGX_E_DEVICE, "%s: %s", what, r ? r->GetErrorString(e) : "RCCL unavailable");
+}
+
+#define HIP_OK(call, what)                              \
+  do {                                                  \
+    hipError_t e_ = (call);                             \
+    if (e_ != hipSuccess) return hip_fail(e_, (what));  \
+  } while (0)
+#define NCCL_OK(call, what)                             \
+  do {                                                  \
+    ncclResult_t e_ = (call);                           \
+    if (e_ != ncclSuccess) return rccl_fail(e_, what);  \
+  } while (0)
+
+constexpr int kFields = 19;  // 13 scalars, loudness_specific, mfcc, amplitude, power, complex real, imag
+
+// Bytes per frame of output array i (mgx_packed_layout numbering).
+uint64_t field_bytes(const mgx_plan_desc& d, int i) {
+  if (i < MGX_NUM_SCALARS) return d.scalar_f64 ? 8 : 4;
+  switch (i) {
+    case 13: return 4ull * d.num_bark_bands;
+    case 14: return 4ull * d.num_mfcc_coeffs;
+    case 15: case 16: return 4ull * (d.buffer_size / 2);
+    default: return 4ull * d.buffer_size;
+  }
+}
+
+bool field_in(uint32_t mask, int i) { return (mask >> (i < 18 ? i : 17)) & 1u; }
+
+void*& field_ptr(mgx_outputs& o, int i) {
+  static void* none = nullptr;
+  if (i < MGX_NUM_SCALARS) return o.scalars[i];
+  switch (i) {
+    case 13: return reinterpret_cast<void*&>(o.loudness_specific);
+    case 14: return reinterpret_cast<void*&>(o.mfcc);
+    case 15: return reinterpret_cast<void*&>(o.amplitude_spectrum);
+    case 16: return reinterpret_cast<void*&>(o.power_spectrum);
+    case 17: return reinterpret_cast<void*&>(o.complex_real);
+    case 18: return reinterpret_cast<void*&>(o.complex_imag);
+    default: return none;
+  }
+}
+
+uint64_t packed_layout(const mgx_plan_desc& d, uint32_t mask, uint64_t nf, uint64_t* off) {
+  uint64_t at = 0;
+  for (int i = 0; i < kFields; ++i) {
+    if (!field_in(mask, i)) {
+      if (off) off[i] = UINT64_MAX;
+      continue;
+    }
+    if (off) off[i] = at;
+    at += (field_bytes(d, i) * nf + 255) / 256 * 256;
+  }
+  return at;
+}
+
+// Outputs of frames [f0, ...) of a structure-of-arrays record.
+mgx_outputs offset_outputs(const mgx_plan_desc& d, const mgx_outputs& o, uint32_t mask, uint64_t f0) {
+  mgx_outputs r{};
+  mgx_outputs src = o;
+  for (int i = 0; i < kFields; ++i)
+    if (field_in(mask, i) && field_ptr(src, i))
+      field_ptr(r, i) = static_cast<unsigned char*>(field_ptr(src, i)) + f0 * field_bytes(d, i);
+  return r;
+}
+
+mgx_outputs packed_outputs(const mgx_plan_desc& d, unsigned char* base, uint32_t mask, uint64_t nf) {
+  uint64_t off[kFields];
+  packed_layout(d, mask, nf, off);
+  mgx_outputs r{};
+  for (int i = 0; i < kFields; ++i)
+    if (off[i] != UINT64_MAX) field_ptr(r, i) = base + off[i];
+  return r;
+}
+
+void chunk_of(uint64_t count, uint32_t nch, uint32_t c, uint64_t* c0, uint64_t* cn) {
+  mgx_shard_range(count, nch, c, c0, cn);
+}
+
+struct Member {
+  uint32_t rank = 0;
+  int device = 0;
+  mgx_plan* plan = nullptr;
+  ncclComm_t comm = nullptr;
+  hipStream_t s_comp = nullptr, s_comm = nullptr;
+  hipEvent_t ev_start = nullptr, ev_comp_done = nullptr, ev_comm_done = nullptr;
+  hipEvent_t ev_comp[2] = {nullptr, nullptr}, ev_sent[2] = {nullptr, nullptr};
+  unsigned char* xfer = nullptr;  // non-root: 2 packed chunk buffers; root: 2 staging slots per peer
+  uint64_t xfer_bytes = 0;
+  float* h_frames = nullptr;       // mgx_group_extract_host: this device's shard
+  uint64_t h_frames_cap = 0;
+  unsigned char* h_out = nullptr;  // root, mgx_group_extract_host: the gathered outputs
+  uint64_t h_out_bytes = 0;
+};
+
+int member_init(Member& m, const mgx_plan_desc& d) {
+  mgx_plan_desc pd = d;
+  pd.device = m.device;
+  int rc = mgx_plan_create(&pd, &m.plan);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(m.device), "hipSetDevice");
+  HIP_OK(hipStreamCreateWithFlags(&m.s_comp, hipStreamNonBlocking), "hipStreamCreate");
+  HIP_OK(hipStreamCreateWithFlags(&m.s_comm, hipStreamNonBlocking), "hipStreamCreate");
+  for (hipEvent_t* e : {&m.ev_start, &m.ev_comp_done, &m.ev_comm_done, &m.ev_comp[0], &m.ev_comp[1], &m.ev_sent[0],
+                        &m.ev_sent[1]})
+    HIP_OK(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
+  return MGX_OK;
+}
+
+void member_free(Member& m) {
+  (void)hipSetDevice(m.device);
+  if (m.s_comp) (void)hipStreamSynchronize(m.s_comp);  // in-flight kernels read the plan's tables
+  if (m.s_comm) (void)hipStreamSynchronize(m.s_comm);
+  if (m.plan) mgx_plan_destroy(m.plan);
+  m.plan = nullptr;
+  if (m.comm) {
+    Rccl* r = rccl();
+    if (r) r->CommDestroy(m.comm);
+  }
+  for (hipEvent_t e : {m.ev_start, m.ev_comp_done, m.ev_comm_done, m.ev_comp[0], m.ev_comp[1], m.ev_sent[0], m.ev_sent[1]})
+    if (e) (void)hipEventDestroy(e);
+  if (m.s_comp) (void)hipStreamDestroy(m.s_comp);
+  if (m.s_comm) (void)hipStreamDestroy(m.s_comm);
+  if (m.xfer) (void)hipFree(m.xfer);
+  if (m.h_frames) (void)hipFree(m.h_frames);
+  if (m.h_out) (void)hipFree(m.h_out);
+  m = Member{};
+}
+
+int ensure(unsigned char** p, uint64_t* cap, uint64_t bytes, const char* what) {
+  if (*cap >= bytes) return MGX_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(p), bytes ? bytes : 1), what);
+  *cap = bytes;
+  return MGX_OK;
+}
+
+}  // namespace
+
+struct mgx_group {
+  mgx_plan_desc d;
+  uint32_t nranks = 0;
+  bool single_process = true;
+  std::vector<Member> m;  // local ranks, in rank order
+};
+
+extern "C" {
+
+int mgx_shard_range(uint64_t total, uint32_t nranks, uint32_t rank, uint64_t* start, uint64_t* count) {
+  if (!start || !count) return fail(MGX_E_INVALID_ARGUMENT, "NULL argument");
+  if (nranks == 0 || rank >= nranks) return fail(MGX_E_INVALID_ARGUMENT, "rank %u of %u", rank, nranks);
+  const uint64_t base = total / nranks, extra = total % nranks;
+  *start = rank * base + std::min<uint64_t>(rank, extra);
+  *count = base + (rank < extra ? 1 : 0);
+  return MGX_OK;
+}
+
+uint64_t mgx_packed_layout(const mgx_plan_desc* desc, uint32_t mask, uint64_t num_frames, uint64_t offsets[19]) {
+  if (!desc) return 0;
+  return packed_layout(*desc, mask, num_frames, offsets);
+}
+
+int mgx_comm_unique_id(void* id, uint64_t id_bytes) {
+  if (!id || id_bytes < sizeof(ncclUniqueId)) return fail(MGX_E_INVALID_ARGUMENT, "id buffer must hold %d bytes", MGX_COMM_ID_BYTES);
+  Rccl* r = rccl();
+  if (!r) return fail(MGX_E_UNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
+  ncclUniqueId u;
+  NCCL_OK(r->GetUniqueId(&u), "ncclGetUniqueId");
+  memcpy(id, &u, sizeof u);
+  return MGX_OK;
+}
+
+int mgx_group_create(const mgx_plan_desc* desc, const int32_t* devices, uint32_t ndev, mgx_group** out) {
+  if (!out) return fail(MGX_E_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  if (!desc || !devices || ndev == 0) return fail(MGX_E_INVALID_ARGUMENT, "a descriptor and at least one device are required");
+  for (uint32_t i = 0; i < ndev; ++i)
+    for (uint32_t j = 0; j < i; ++j)
+      if (devices[i] == devices[j]) return fail(MGX_E_INVALID_ARGUMENT, "device %d listed twice", devices[i]);
+  auto* g = new mgx_group();
+  g->d = *desc;
+  g->nranks = ndev;
+  g->single_process = true;
+  g->m.resize(ndev);
+  int rc = MGX_OK;
+  for (uint32_t i = 0; i < ndev && !rc; ++i) {
+    g->m[i].rank = i;
+    g->m[i].device = devices[i];
+    rc = member_init(g->m[i], *desc);
+  }
+  if (!rc && ndev > 1) {
+    Rccl* r = rccl();
+    if (!r) {
+      rc = fail(MGX_E_UNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
+    } else {
+      std::vector<ncclComm_t> comms(ndev);
+      std::vector<int> devs(devices, devices + ndev);
+      ncclResult_t e = r->CommInitAll(comms.data(), (int)ndev, devs.data());
+      if (e != ncclSuccess) rc = rccl_fail(e, "ncclCommInitAll");
+      else for (uint32_t i = 0; i < ndev; ++i) g->m[i].comm = comms[i];
+    }
+  }
+  if (rc) {
+    mgx_group_destroy(g);
+    return rc;
+  }
+  *out = g;
+  return MGX_OK;
+}
+
+int mgx_group_create_rank(const mgx_plan_desc* desc, const void* unique_id, uint32_t nranks, uint32_t rank,
+                          mgx_group** out) {
+  if (!out) return fail(MGX_E_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  if (!desc || nranks == 0 || rank >= nranks) return fail(MGX_E_INVALID_ARGUMENT, "rank %u of %u", rank, nranks);
+  if (nranks > 1 && !unique_id) return fail(MGX_E_INVALID_ARGUMENT, "unique_id is NULL");
+  auto* g = new mgx_group();
+  g->d = *desc;
+  g->nranks = nranks;
+  g->single_process = nranks == 1;
+  g->m.resize(1);
+  g->m[0].rank = rank;
+  g->m[0].device = desc->device;
+  int rc = member_init(g->m[0], *desc);
+  if (!rc && nranks > 1) {
+    Rccl* r = rccl();
+    if (!r) {
+      rc = fail(MGX_E_UNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
+    } else {
+      ncclUniqueId u;
+      memcpy(&u, unique_id, sizeof u);
+      (void)hipSetDevice(desc->device);
+      ncclResult_t e = r->CommInitRank(&g->m[0].comm, (int)nranks, u, (int)rank);
+      if (e != ncclSuccess) rc = rccl_fail(e, "ncclCommInitRank");
+    }
+  }
+  if (rc) {
+    mgx_group_destroy(g);
+    return rc;
+  }
+  *out = g;
+  return MGX_OK;
+}
+
+int mgx_group_destroy(mgx_group* g) {
+  if (!g) return MGX_OK;
+  for (Member& m : g->m) member_free(m);
+  delete g;
+  return MGX_OK;
+}
+
+int mgx_group_info(const mgx_group* g, uint32_t* nranks, uint32_t* first_local, uint32_t* num_local) {
+  if (!g) return fail(MGX_E_INVALID_ARGUMENT, "group is NULL");
+  if (nranks) *nranks = g->nranks;
+  if (first_local) *first_local = g->m.empty() ? 0 : g->m[0].rank;
+  if (num_local) *num_local = (uint32_t)g->m.size();
+  return MGX_OK;
+}
+
+int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uint64_t* counts,
+                             const mgx_outputs* root_out, uint32_t mask, uint32_t nch, void* const* streams) {
+  if (!g || !frames || !counts) return fail(MGX_E_INVALID_ARGUMENT, "NULL argument");
+  if (mask & ~MGX_OUT_ALL_MASK) return fail(MGX_E_INVALID_ARGUMENT, "unknown output bits in mask 0x%x", mask);
+  const mgx_plan_desc& d = g->d;
+  const uint32_t R = g->nranks;
+  const uint64_t N = d.buffer_size;
+  std::vector<uint64_t> start(R);
+  uint64_t total = 0, most = 0;
+  for (uint32_t r = 0; r < R; ++r) {
+    start[r] = total;
+    total += counts[r];
+    most = std::max(most, counts[r]);
+  }
+  const bool root_local = g->m[0].rank == 0;
+  if (root_local) {
+    if (!root_out) return fail(MGX_E_INVALID_ARGUMENT, "root outputs are NULL on the root");
+    mgx_outputs chk = *root_out;
+    for (int i = 0; i < kFields; ++i)
+      if (field_in(mask, i) && !field_ptr(chk, i)) return fail(MGX_E_INVALID_ARGUMENT, "output %d is in the mask but NULL", i);
+  }
+  for (size_t i = 0; i < g->m.size(); ++i)
+    if (counts[g->m[i].rank] && !frames[i]) return fail(MGX_E_INVALID_ARGUMENT, "frames of local rank %zu are NULL", i);
+  // pipeline depth: about 64 Ki frames per chunk, at most 8 chunks
+  if (nch == 0) nch = (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, (most + 65535) / 65536));
+  if (R == 1) nch = std::max<uint32_t>(nch, 1);
+  uint64_t cmax = 0;
+  for (uint32_t r = 0; r < R; ++r) {
+    uint64_t c0, cn;
+    chunk_of(counts[r], nch, 0, &c0, &cn);  // chunk 0 is the largest
+    cmax = std::max(cmax, cn);
+  }
+  const uint64_t slot = packed_layout(d, mask, cmax, nullptr);
+  // buffers: non-root 2 packed chunks; root 2 staging slots per peer
+  for (Member& m : g->m) {
+    HIP_OK(hipSetDevice(m.device), "hipSetDevice");
+    const uint64_t need = R == 1 ? 0 : (m.rank == 0 ? 2 * slot * (R - 1) : 2 * slot);
+    int rc = ensure(&m.xfer, &m.xfer_bytes, need, "hipMalloc(transfer buffers)");
+    if (rc) return rc;
+  }
+  // order after the callers' streams
+  for (size_t i = 0; i < g->m.size(); ++i) {
+    Member& m = g->m[i];
+    HIP_OK(hipSetDevice(m.device), "hipSetDevice");
+    hipStream_t us = streams ? static_cast<hipStream_t>(streams[i]) : nullptr;
+    HIP_OK(hipEventRecord(m.ev_start, us), "hipEventRecord");
+    HIP_OK(hipStreamWaitEvent(m.s_comp, m.ev_start, 0), "hipStreamWaitEvent");
+    HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_start, 0), "hipStreamWaitEvent");
+  }
+  Rccl* rc_ = R > 1 ? rccl() : nullptr;
+  if (R > 1 && !rc_) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
+  for (uint32_t c = 0; c < nch; ++c) {
+    const int sl = (int)(c & 1);
+    // extraction of chunk c on every local rank
+    for (Member& m : g->m) {
+      uint64_t c0, cn;
+      chunk_of(counts[m.rank], nch, c, &c0, &cn);
+      HIP_OK(hipSetDevice(m.device), "hipSetDevice");
+      const float* src = frames[&m - &g->m[0]] + c0 * N;
+      if (m.rank == 0) {
+        if (cn) {
+          const mgx_outputs o = offset_outputs(d, *root_out, mask, start[0] + c0);
+          int rc = mgx_extract_device(m.plan, src, cn, &o, m.s_comp);
+          if (rc) return rc;
+        }
+      } else {
+        if (c >= 2) HIP_OK(hipStreamWaitEvent(m.s_comp, m.ev_sent[sl], 0), "hipStreamWaitEvent");
+        if (cn) {
+          const mgx_outputs o = packed_outputs(d, m.xfer + sl * slot, mask, cn);
+          int rc = mgx_extract_device(m.plan, src, cn, &o, m.s_comp);
+          if (rc) return rc;
+        }
+        HIP_OK(hipEventRecord(m.ev_comp[sl], m.s_comp), "hipEventRecord");
+        HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_comp[sl], 0), "hipStreamWaitEvent");
+      }
+    }
+    if (R == 1) continue;
+    // transfers of chunk c (one group: in single-process mode it spans every device)
+    NCCL_OK(rc_->GroupStart(), "ncclGroupStart");
+    for (Member& m : g->m) {
+      if (m.rank == 0) {
+        for (uint32_t p = 1; p < R; ++p) {
+          uint64_t c0, cn;
+          chunk_of(counts[p], nch, c, &c0, &cn);
+          if (!cn) continue;
+          unsigned char* st = m.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot;
+          NCCL_OK(rc_->Recv(st, packed_layout(d, mask, cn, nullptr), ncclUint8, (int)p, m.comm, m.s_comm), "ncclRecv");
+        }
+      } else {
+        uint64_t c0, cn;
+        chunk_of(counts[m.rank], nch, c, &c0, &cn);
+        if (cn) NCCL_OK(rc_->Send(m.xfer + sl * slot, packed_layout(d, mask, cn, nullptr), ncclUint8, 0, m.comm, m.s_comm), "ncclSend");
+      }
+    }
+    NCCL_OK(rc_->GroupEnd(), "ncclGroupEnd");
+    for (Member& m : g->m) {
+      HIP_OK(hipSetDevice(m.device), "hipSetDevice");
+      if (m.rank != 0) {
+        HIP_OK(hipEventRecord(m.ev_sent[sl], m.s_comm), "hipEventRecord");
+        continue;
+      }
+      // scatter each peer's chunk into the root's outputs (ordered after its receive)
+      for (uint32_t p = 1; p < R; ++p) {
+        uint64_t c0, cn;
+        chunk_of(counts[p], nch, c, &c0, &cn);
+        if (!cn) continue;
+        uint64_t off[kFields];
+        packed_layout(d, mask, cn, off);
+        mgx::UnpackArgs ua{};
+        ua.src = m.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot;
+        mgx_outputs dst = offset_outputs(d, *root_out, mask, start[p] + c0);
+        for (int i = 0; i < kFields; ++i) {
+          if (off[i] == UINT64_MAX) continue;
+          ua.src_off[ua.nseg] = off[i];
+          ua.dst[ua.nseg] = field_ptr(dst, i);
+          ua.dwords[ua.nseg] = field_bytes(d, i) * cn / 4;
+          ++ua.nseg;
+        }
+        HIP_OK(mgx::launch_unpack(ua, m.s_comm), "unpack kernel launch");
+      }
+    }
+  }
+  // the callers' streams wait for the extraction and the gather
+  for (size_t i = 0; i < g->m.size(); ++i) {
+    Member& m = g->m[i];
+    HIP_OK(hipSetDevice(m.device), "hipSetDevice");
+    hipStream_t us = streams ? static_cast<hipStream_t>(streams[i]) : nullptr;
+    HIP_OK(hipEventRecord(m.ev_comp_done, m.s_comp), "hipEventRecord");
+    HIP_OK(hipEventRecord(m.ev_comm_done, m.s_comm), "hipEventRecord");
+    HIP_OK(hipStreamWaitEvent(us, m.ev_comp_done, 0), "hipStreamWaitEvent");
+    HIP_OK(hipStreamWaitEvent(us, m.ev_comm_done, 0), "hipStreamWaitEvent");
+  }
+  return MGX_OK;
+}
+
+int mgx_group_extract_host(mgx_group* g, const float* frames, uint64_t nframes, const mgx_outputs* o) {
+  if (!g || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL group or outputs");
+  if (!g->single_process || g->m.size() != g->nranks)
+    return fail(MGX_E_UNSUPPORTED, "host batches need a single-process group (mgx_group_create)");
+  if (nframes == 0) return MGX_OK;
+  if (!frames) return fail(MGX_E_INVALID_ARGUMENT, "frames is NULL");
+  if ((o->complex_real == nullptr) != (o->complex_imag == nullptr))
+    return fail(MGX_E_INVALID_ARGUMENT, "complex_real and complex_imag must be given together");
+  const mgx_plan_desc& d = g->d;
+  const uint32_t R = g->nranks;
+  const uint64_t N = d.buffer_size;
+  mgx_outputs oh = *o;
+  uint32_t mask = 0;
+  for (int i = 0; i < 18; ++i)
+    if (field_ptr(oh, i)) mask |= 1u << i;
+  std::vector<uint64_t> start(R), cnt(R);
+  for (uint32_t r = 0; r < R; ++r) mgx_shard_range(nframes, R, r, &start[r], &cnt[r]);
+  // shards to the devices, one host thread per device (parallel PCIe copies)
+  std::vector<int> rcs(R, MGX_OK);
+  std::vector<std::string> errs(R);
+  std::vector<std::thread> th;
+  for (uint32_t r = 0; r < R; ++r) {
+    th.emplace_back([&, r]() {
+      Member& m = g->m[r];
+      int rc = MGX_OK;
+      hipError_t e = hipSetDevice(m.device);
+      uint64_t cap = m.h_frames_cap * 4;
+      unsigned char* p = reinterpret_cast<unsigned char*>(m.h_frames);
+      if (e == hipSuccess) rc = ensure(&p, &cap, cnt[r] * N * 4, "hipMalloc(shard frames)");
+      m.h_frames = reinterpret_cast<float*>(p);
+      m.h_frames_cap = cap / 4;
+      if (e == hipSuccess && !rc && cnt[r])
+        e = hipMemcpy(m.h_frames, frames + start[r] * N, cnt[r] * N * 4, hipMemcpyHostToDevice);
+      if (e != hipSuccess) rc = hip_fail(e, "hipMemcpy(shard frames)");
+      if (rc) errs[r] = mgx_last_error();
+      rcs[r] = rc;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (uint32_t r = 0; r < R; ++r)
+    if (rcs[r]) return fail(rcs[r], "%s", errs[r].c_str());
+  // the gathered record on the root device
+  Member& root = g->m[0];
+  HIP_OK(hipSetDevice(root.device), "hipSetDevice");
+  uint64_t off[kFields];
+  const uint64_t bytes = packed_layout(d, mask, nframes, off);
+  int rc = ensure(&root.h_out, &root.h_out_bytes, bytes, "hipMalloc(gathered outputs)");
+  if (rc) return rc;
+  mgx_outputs dev = packed_outputs(d, root.h_out, mask, nframes);
+  std::vector<const float*> fr(R);
+  for (uint32_t r = 0; r < R; ++r) fr[r] = g->m[r].h_frames;
+  rc = mgx_group_extract_device(g, fr.data(), cnt.data(), &dev, mask, 0, nullptr);
+  if (rc) return rc;
+  for (Member& m : g->m) {
+    HIP_OK(hipSetDevice(m.device), "hipSetDevice");
+    HIP_OK(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  }
+  HIP_OK(hipSetDevice(root.device), "hipSetDevice");
+  for (int i = 0; i < kFields; ++i) {
+    if (off[i] == UINT64_MAX) continue;
+    HIP_OK(hipMemcpy(field_ptr(oh, i), root.h_out + off[i], field_bytes(d, i) * nframes, hipMemcpyDeviceToHost),
+           "hipMemcpy(outputs)");
+  }
+  return MGX_OK;
+}
+
+}  // extern "C"

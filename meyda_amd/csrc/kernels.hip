@@ -253,6 +253,14 @@ __device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))
 #endif
 }
 
+// Static instruction accounting (tools/isa_phases.py): -DMGX_MARKS puts an assembly comment
+// at each phase boundary; the default build has none.
+#ifdef MGX_MARKS
+#define MGX_MARK(tag) asm volatile(";mgxmark " #tag)
+#else
+#define MGX_MARK(tag) ((void)0)
+#endif
+
 // Wave-level LDS ordering (no global-memory fence: in-flight prefetch loads stay in flight).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -507,6 +515,7 @@ __device__ __forceinline__ void exchange(float2 (&v)[Geo<N>::R], int lp_prev, in
   using G = Geo<N>;
   using PG = PassGeo<N>;
   const int bprev = phys<N>(lp_prev), bcur = phys<N>(lp_cur);
+  MGX_MARK(xchg_begin);
   prio_hi<1>();
   wave_sync();
 #pragma unroll
@@ -515,6 +524,7 @@ __device__ __forceinline__ void exchange(float2 (&v)[Geo<N>::R], int lp_prev, in
 #pragma unroll
   for (int r = 0; r < G::R; ++r) v[r] = buf[bcur + phys<N>(PG::rpart(P, r))];
   prio_lo<1>();
+  MGX_MARK(xchg_end);
 }
 
 template <int N, int P, bool FAITH, bool TAME>
@@ -864,6 +874,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
   };
   if (!ap->need_spectrum) prefetch_next();  // time-only features: no table loads follow
+  MGX_MARK(energy_zcr);
   // rms.js / energy.js: sum of squares; zcr.js: sign changes of adjacent samples,
   // `x >= 0` vs `x < 0` (so -0 is non-negative and NaN never counts).
   // Sum of squares as packed float32 FMAs over pairs of chunks; zcr from one ballot per
@@ -935,6 +946,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #else
   const bool tame = !__ballot(!(e32 <= 0x1p100f));
 #endif
+  MGX_MARK(window);
 
   // src/meyda.js:158-168: windowed[i] = sig[i] * w[i], stored to Float32Array
   // (the exact double product rounded once == a float32 multiply).
@@ -967,6 +979,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
         v[r].y = kSf * (x[c] - x[c + R]);
       }
     }
+    MGX_MARK(stage0_done);
     GTw tw = gbl(ap->t.tw);
     GTwf twf = gbl(ap->t.twf);
     GTw twm = gbl(ap->t.twm);
@@ -980,12 +993,14 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     if constexpr (FAITH) {
       // pass 0 has no mixed pairs; the later passes take the tame form when they can
       run_stages<N, 0, 0, FAITH, false>(v, lpf[0], tw, twf, twm);
+      MGX_MARK(pass0_done);
       if (tame) run_passes<N, 1, FAITH, true>(v, lpf, buf, tw, twf, twm);
       else run_passes<N, 1, FAITH, false>(v, lpf, buf, tw, twf, twm);
     } else {
       run_passes<N, 0, FAITH, false>(v, lpf, buf, tw, twf, twm);
     }
 #endif
+    MGX_MARK(fft_done);
     const bool want_cplx = ap->out.complex_real != nullptr;
     // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
     float ar[R];
@@ -1015,6 +1030,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       const bool dc = (PG::rpart(G::NPASS - 1, r) == 0) && dc_lane;
       if (dc) ar[r] = fabsf(v[r].x);  // slot 0 packs (X[0], X[N/2]), both real
     }
+    MGX_MARK(amp_done);
     wave_sync();  // the last exchange's reads are done: the slot buffer is free
     if (want_cplx) {
       // natural-order half spectrum X[0..N/2] in the slot buffer
@@ -1067,6 +1083,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) av[jj] = amp[pa(R * lane + jj)];
   prio_lo<2>();
+  MGX_MARK(amp_row_done);
   // The moment and log sums only as far as a feature reads them (need_mom: 0 none, 1 S1 for
   // centroid / slope, 2 S1..S4 and sum log2 a); the amplitude total T0 always (S0, rolloff,
   // the non-finite test). SUB: a feature subset, the flags are read at run time; otherwise
@@ -1111,6 +1128,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #pragma unroll
     for (int jj = 0; jj < R; ++jj) T0 += (double)av[jj];
   }
+  MGX_MARK(moments_done);
   wave_sync();  // every lane has read the amplitude row: the buffer takes the prefix sums next
   FrameRec& rec = recs[fb];
   // Moments S1..S4 (bin-offset polynomial shift of the local partials) and sum log2 a:
@@ -1160,6 +1178,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
   }
   const int roll_m = (total > thr) ? cnt - 1 : L;
+  MGX_MARK(prefix_done);
   // The lane's mel records, then (G::PF == 2) the next frame: issued after the last table
   // load this frame waits on before them, so no wait of this frame is held up by the
   // prefetch; the band and mel sums, the moment finish and phase 2 run while it is in
@@ -1186,6 +1205,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       rec.ln2sum = l2;
     }
   }
+  MGX_MARK(prefetch_issued);
   if (need_prefix && lane < kBark) {
     const int lb = opaque(lane);  // (an address kept live across the frame loop spills at N = 2048)
     rec.band[lb] = pbuf[pd(klim[lb + 1])] - pbuf[pd(klim[lb])];  // limits staged in LDS
@@ -1200,11 +1220,13 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // the reference's own summation: bark bands bin by bin in double (loudness.js:47-66),
   // mel bands over all bins in reference order (mfcc.js:53-62).
   // (total = sum of the amplitudes in double: non-finite iff some amplitude is.)
+  MGX_MARK(bands_done);
   if (!(total < __builtin_huge_val())) {
     nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
   } else if (ABL_ON(MELSCAN) && ap->need_mfcc) {
     mel_energies<N>(ap, av, lane, buf, rec, mt);
   }
+  MGX_MARK(mel_done);
   if (kMomLds && need_mom) {
     wave_sync();
     const int row = lane < 40 ? lane >> 3 : 0;
@@ -1218,6 +1240,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #else
   prefetch_next();  // (timing ablation: the frames are still read)
 #endif
+  MGX_MARK(frame_end);
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
 }
 
@@ -1398,6 +1421,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     // ------------------------------------------------------------- phase 2
     // Lane ids and the argument pointer are re-derived so that nothing phase 2 needs is
     // hoisted out of the batch loop (it would stay live across the FFT).
+    MGX_MARK(phase2_start);
     {
       KArgs* q = args_ptr();
       const int l2 = opaque(lane);
@@ -1440,6 +1464,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
           }
         }
       }
+      MGX_MARK(loud2_done);
       if (ABL_ON(COMB) && q->need_spectrum && q->need_mfcc) {
         // mfcc.js:64 Math.log of the band energies, stored to Float32Array
         const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
@@ -1453,6 +1478,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     {
       KArgs* q = args_ptr();
       const int l2 = opaque(lane);
+      MGX_MARK(ln_done);
       if (ABL_ON(DCT) && q->need_spectrum && q->need_mfcc) {
         const int nc = q->ncoef, nfilt = q->nfilt;
 #ifndef MGX_DCT_MFMA
@@ -1501,6 +1527,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         }
 #endif
       }
+      MGX_MARK(dct_done);
       // the other scalar features: one lane per (feature, frame)
       for (int i = l2; ABL_ON(FIN) && i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {
         const int sc = i / FPW, fb = i % FPW;
@@ -1515,6 +1542,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
 #ifdef MGX_ABL_NO_PHASE2
     }
 #endif
+    MGX_MARK(phase2_end);
     wave_sync();  // records and slot buffer are reused by the next batch
   }
 }
@@ -1561,6 +1589,19 @@ __global__ void pcm_decode_kernel(const unsigned char* __restrict__ pcm, uint64_
     }
     out[i] = v;
   }
+}
+
+// Packed transfer buffer -> the root's structure-of-arrays outputs (group.cpp). One
+// workgroup row per segment (blockIdx.y); dword copies: every field is a whole number of
+// dwords per frame, and a shard's destination offset is only dword-aligned.
+__global__ void unpack_kernel(UnpackArgs a) {
+  const int s = blockIdx.y;
+  if (s >= a.nseg) return;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(a.src + a.src_off[s]);
+  uint32_t* dst = static_cast<uint32_t*>(a.dst[s]);
+  const uint64_t n = a.dwords[s];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
 }
 
 template <int N, bool FAITH, bool LITERAL, bool SUB = false>
@@ -1648,6 +1689,16 @@ hipError_t launch_pcm_decode(const void* pcm, uint64_t count, uint32_t format, u
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(pcm_decode_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
                      static_cast<const unsigned char*>(pcm), count, format, bps * channels, bps * channel, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack(const UnpackArgs& a, hipStream_t stream) {
+  uint64_t most = 0;
+  for (int i = 0; i < a.nseg; ++i) most = a.dwords[i] > most ? a.dwords[i] : most;
+  if (a.nseg == 0 || most == 0) return hipSuccess;
+  uint64_t bx = (most + 1023) / 1024;
+  if (bx > 256) bx = 256;
+  hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)bx, (unsigned)a.nseg), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -48,6 +48,10 @@ struct KernelArgs {
   int need_prefix;       // rolloff or loudness: the prefix row (rolloff count, bark band sums)
 };
 
+// Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int hip_fail(hipError_t e, const char* what);
+
 // Launchers (kernels.hip).
 hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, int grid,
                           hipStream_t stream);
@@ -55,6 +59,17 @@ hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t firs
                         hipStream_t stream);
 hipError_t launch_pcm_decode(const void* pcm, uint64_t count, uint32_t format, uint32_t channels,
                              uint32_t channel, float* out, hipStream_t stream);
+// Scatter of one packed transfer buffer into the root's outputs (group.cpp): segment i
+// copies dwords[i] dwords from src + src_off[i] to dst[i].
+constexpr int kMaxSegs = 19;
+struct UnpackArgs {
+  const unsigned char* src;
+  uint64_t src_off[kMaxSegs];
+  void* dst[kMaxSegs];
+  uint64_t dwords[kMaxSegs];
+  int nseg;
+};
+hipError_t launch_unpack(const UnpackArgs& a, hipStream_t stream);
 size_t extract_lds_bytes(int n, int ncoef, int nfilt);
 int frames_per_batch(int n);
 int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt);  // resident workgroups per CU

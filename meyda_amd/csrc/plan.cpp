@@ -18,9 +18,10 @@
 #include "mgx_internal.h"
 
 namespace {
-
 thread_local std::string g_last_error;
+}  // namespace
 
+namespace mgx {
 int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
@@ -35,6 +36,11 @@ int hip_fail(hipError_t e, const char* what) {
   const int code = (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? MGX_E_OUT_OF_MEMORY : MGX_E_DEVICE;
   return fail(code, "%s: %s", what, hipGetErrorString(e));
 }
+}  // namespace mgx
+
+namespace {
+using mgx::fail;
+using mgx::hip_fail;
 
 const uint64_t kHostChunk = 65536;              // frames per host-staging chunk
 const double kJsPi = 3.141592653589793;        // Math.PI

@@ -16,6 +16,8 @@
 //                                   decoded on the device: decodeAudioData's scaling)
 //   Meyda.readWav(wavBytes)         the header: {pcmFormat, channels, sampleRate, sampleFrames, ...}
 //   flush()                         deliver buffered callbacks now (options.batchFrames > 1)
+//   options.devices = [0, 1, ...]   shard batches over several GPUs; the feature records are
+//                                   gathered to the first one by RCCL (one plan per device)
 //
 // Streaming (start/stop, src/meyda.js:69-91,233-241): with options.batchFrames = K > 1
 // the buffers pushed by process() are queued and extracted K at a time in one launch;
@@ -105,6 +107,9 @@ class Meyda {
       precision: this.options.precision, mode: this.options.mode,
       numMelBands: this.options.numMelBands, numMfccCoeffs: this.options.numMfccCoeffs,
       device: this.options.device, scalarF64: 1,
+      // options.devices = [d0, d1, ...]: every batch is sharded over the devices and the
+      // per-frame features are gathered to d0 over xGMI (RCCL), include/meyda_gpu.h mgx_group_*
+      ...(Array.isArray(this.options.devices) ? { devices: this.options.devices } : {}),
     });
   }
 

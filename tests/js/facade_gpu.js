@@ -199,6 +199,23 @@ check('plan handle collected while an async job runs (no use-after-free)', () =>
   });
 });
 
+check('options.devices: batches through a device group equal the single-device plan', () => {
+  const F = 77;
+  const x = g.input.subarray(0, F * 512);
+  const one = new Meyda(ctx, null, 512);
+  const grp = new Meyda(ctx, null, 512, null, { devices: [0] });
+  const a = one.getBatch(ALL, x);
+  const b = grp.getBatch(ALL, x);
+  for (const k of Object.keys(a)) assert.deepStrictEqual(Array.from(b[k]), Array.from(a[k]), k);
+  grp.process(frameOf(g, 3));
+  assert.strictEqual(grp.get('zcr'), g.scalars[3 * S + 2]);
+  return grp.getBatchAsync(['rms'], x).then((r) => {
+    assert.deepStrictEqual(Array.from(r.rms), Array.from(a.rms));
+    one.dispose();
+    grp.dispose();
+  });
+});
+
 (async () => {
   for (const [name, fn] of checks) {
     await fn();

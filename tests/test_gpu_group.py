@@ -1,0 +1,105 @@
+"""Multi-device groups on the GPU (include/meyda_gpu.h "Multi-device groups"): a one-rank
+group, single-process (mgx_group_create) and per-process (mgx_group_create_rank), run
+through the chunked extraction path and must be byte-identical to one plan's extraction;
+with two or more devices visible, the RCCL gather of a real multi-device group too.
+Frame independence (src/meyda.js:69-91) makes every chunking and sharding legal."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x6D657964
+FEATS = ["rms", "energy", "zcr", "spectralCentroid", "spectralFlatness", "spectralSlope",
+         "spectralRolloff", "spectralSpread", "spectralSkewness", "spectralKurtosis", "loudness",
+         "perceptualSpread", "perceptualSharpness", "mfcc", "amplitudeSpectrum", "powerSpectrum",
+         "complexSpectrum"]
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from meyda_amd import capi
+    if capi.device_count() == 0:
+        pytest.fail("no GPU visible to libmeyda_gpu.so")
+    return capi
+
+
+def _frames(capi, F, n, first=0):
+    import torch
+    x = torch.empty(F, n, dtype=torch.float32, device="cuda")
+    capi.synth_frames_device(x, SEED, first_frame=first)
+    return x
+
+
+@pytest.mark.parametrize("mode", ["devices", "rank"])
+@pytest.mark.parametrize("nch", [1, 3, 8])
+def test_one_rank_group_equals_plan(capi, mode, nch):
+    import torch
+    n, F = 1024, 5000
+    x = _frames(capi, F, n)
+    plan = capi.Plan(buffer_size=n, scalar_f64=True)
+    want = plan.extract_torch(x, FEATS)
+    if mode == "devices":
+        g = capi.Group(buffer_size=n, devices=[0], scalar_f64=True)
+    else:
+        g = capi.Group(buffer_size=n, rank=0, nranks=1, device=0, scalar_f64=True)
+    assert (g.nranks, g.first_local, g.num_local) == (1, 0, 1)
+    got, o = plan.alloc_outputs(F, FEATS)
+    for v in got.values():
+        v.fill_(float("nan"))
+    stream = torch.cuda.current_stream().cuda_stream
+    g.extract_device([x.data_ptr()], [F], o, capi.output_mask(o), num_chunks=nch, streams=[stream])
+    torch.cuda.synchronize()
+    for k in want:
+        assert torch.equal(got[k].view(torch.int32) if got[k].dtype == torch.float32 else got[k].view(torch.int64),
+                           want[k].view(torch.int32) if want[k].dtype == torch.float32 else want[k].view(torch.int64)), k
+    g.close()
+
+
+def test_group_host_batch_equals_plan(capi):
+    n, F = 512, 3001
+    x = _frames(capi, F, n).cpu().numpy()
+    feats = ["rms", "zcr", "spectralCentroid", "loudness", "mfcc", "amplitudeSpectrum"]
+    want = capi.Plan(buffer_size=n).extract(x, feats)
+    g = capi.Group(buffer_size=n, devices=[0])
+    got = g.extract(x, feats)
+    for k in want:
+        assert np.array_equal(got[k].view(np.uint32), want[k].view(np.uint32)), k
+
+
+def test_group_argument_errors(capi):
+    with pytest.raises(capi.MgxError):
+        capi.Group(buffer_size=512, devices=[0, 0])  # a device twice
+    with pytest.raises(capi.MgxError):
+        capi.Group(buffer_size=512, rank=1, nranks=1)
+    g = capi.Group(buffer_size=512, devices=[0])
+    with pytest.raises(capi.MgxError):  # the root's outputs must hold every masked field
+        g.extract_device([0], [0], capi.Outputs(), capi.OUT_MFCC)
+
+
+def test_multi_device_gather(capi):
+    """Two or more devices in one process: shards, chunked RCCL gather to device 0."""
+    import torch
+    ndev = capi.device_count()
+    if ndev < 2:
+        pytest.skip("one device visible: the RCCL gather needs two (covered on the multi-GPU node)")
+    devs = list(range(min(ndev, 4)))
+    n, F = 1024, 40000
+    g = capi.Group(buffer_size=n, devices=devs, scalar_f64=True)
+    counts = [capi.shard_range(F, len(devs), r)[1] for r in range(len(devs))]
+    starts = [capi.shard_range(F, len(devs), r)[0] for r in range(len(devs))]
+    xs = []
+    for d, s, c in zip(devs, starts, counts):
+        with torch.cuda.device(d):
+            xs.append(_frames(capi, c, n, first=s))
+    plan = capi.Plan(buffer_size=n, scalar_f64=True)
+    feats = ["rms", "spectralKurtosis", "loudness", "mfcc", "amplitudeSpectrum"]
+    got, o = plan.alloc_outputs(F, feats)
+    for dd in devs:
+        torch.cuda.synchronize(dd)
+    g.extract_device([t.data_ptr() for t in xs], counts, o, capi.output_mask(o), num_chunks=4)
+    for dd in devs:
+        torch.cuda.synchronize(dd)
+    want = plan.extract_torch(_frames(capi, F, n), feats)
+    torch.cuda.synchronize()
+    for k in want:
+        assert torch.equal(got[k], want[k]), k
