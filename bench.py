@@ -52,7 +52,8 @@ def parse():
     ap.add_argument("--frames", type=int, default=262144, help="frames per GPU per step")
     ap.add_argument("--precision", default="faithful", choices=["faithful", "fast"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0,
+                    help="CPU baseline: seconds of the multi-thread run (1 thread and the C port: a third)")
     ap.add_argument("--also-fast", action="store_true", help="report the fp32 mode alongside")
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: time the shards alone, without the RCCL gather to rank 0")
@@ -60,11 +61,13 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n, seconds):
-    """Time the CPU oracle (C restatement of the reference path) on host cores."""
+CPU_THREADS = 16  # the GPU box's CPU share per GPU (os.cpu_count() there is the whole machine)
+
+
+def cpu_port_c(n, seconds, threads):
+    """Secondary: the C restatement (oracle/meyda_oracle.c) on the same cores."""
     from oracle import oracle
     oracle.lib()
-    threads = min(16, os.cpu_count() or 1)
     per = 256
     x = oracle.synth_frames(capi_seed(), 0, per * threads, n)
 
@@ -80,11 +83,38 @@ def cpu_baseline(n, seconds):
         t0 = time.perf_counter()
         res = list(ex.map(work, range(threads)))
         wall = time.perf_counter() - t0
-    frames = sum(r[0] for r in res)
-    one = work(0)
-    return {"value": frames / wall, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": "%d frames (N=%d, all features, seeded noise) over %.1f s on %d threads; "
-                      "1 thread: %.0f frames/s" % (frames, n, wall, threads, one[0] / one[1])}
+    return {"value": sum(r[0] for r in res) / wall, "unit": "frames/s", "cores": threads, "kind": "port-c"}
+
+
+def cpu_baseline(n, seconds):
+    """The reference's Node/jsfft CPU path as the build's JavaScript restatement
+    (oracle/js/meyda_cpu.js, bit-exact to the reference's golden outputs), in the
+    reference's per-buffer structure, timed on this host with 1 and CPU_THREADS
+    worker_threads on the seeded stream; the C port beside it."""
+    import shutil
+    import subprocess
+    threads = min(CPU_THREADS, os.cpu_count() or 1)
+    js = os.path.join(ROOT, "oracle", "js", "bench_cpu.js")
+    out = {"unit": "frames/s", "kind": "js-restatement"}
+    if shutil.which("node"):
+        def run(t, secs):
+            r = subprocess.run(["node", js, str(n), str(secs), str(t), "reference"], capture_output=True, text=True,
+                               timeout=120 + 4 * secs, check=True)
+            return json.loads(r.stdout.strip().splitlines()[-1])
+        one = run(1, max(1.0, seconds / 3))
+        many = run(threads, seconds)
+        out.update({"value": many["value"], "cores": threads, "cpu_model": many["cpu_model"],
+                    "logical_cpus": many["logical_cpus"], "node": many["node"], "one_thread": one["value"],
+                    "sample": "%d frames (N=%d, all features, seeded noise, the reference's per-buffer structure) "
+                              "over %.1f s on %d worker_threads; 1 thread: %.0f frames/s"
+                              % (many["frames"], n, many["seconds"], threads, one["value"])})
+    else:  # no Node on this host: the C port stands in
+        out.update({"kind": "port", "value": None, "note": "node not found"})
+    out["port_c"] = cpu_port_c(n, max(1.0, seconds / 3), threads)
+    if out.get("value") is None:
+        out["value"] = out["port_c"]["value"]
+        out["cores"] = threads
+    return out
 
 
 def capi_seed():
