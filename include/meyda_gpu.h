@@ -44,7 +44,8 @@
 extern "C" {
 #endif
 
-#define MGX_ABI_VERSION 2  /* 2: mgx_extract_host_pcm takes the PCM byte count */
+#define MGX_ABI_VERSION 2  /* 2: mgx_extract_host_pcm takes the PCM byte count; mgx_plan_desc.flags;
+                              multi-device groups */
 
 typedef enum mgx_status {
   MGX_OK = 0,
@@ -112,7 +113,13 @@ typedef struct mgx_plan_desc {
   uint32_t num_mfcc_coeffs;  /* 13 (mfcc.js:71) */
   uint32_t scalar_f64;       /* 0: scalar outputs are float32 arrays, 1: float64 */
   int32_t device;            /* HIP device ordinal */
+  uint32_t flags;            /* MGX_FLAG_* */
 } mgx_plan_desc;
+
+/* mgx_plan_desc.flags */
+#define MGX_FLAG_DCT_SEQUENTIAL 1u  /* mfcc.js:85-93 DCT as VALU FMAs in the reference's sequential
+                                        order instead of the FP64 matrix cores (the default: same
+                                        exact products, f64 sums in 4-band blocks) */
 
 typedef struct mgx_plan mgx_plan;
 

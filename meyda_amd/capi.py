@@ -38,6 +38,7 @@ EXPORTS = ["mgx_plan_desc_init", "mgx_plan_create", "mgx_plan_destroy", "mgx_pla
            "mgx_group_create_rank", "mgx_group_destroy", "mgx_group_info", "mgx_group_extract_device",
            "mgx_group_extract_host"]
 COMM_ID_BYTES = 128
+FLAG_DCT_SEQUENTIAL = 1  # mgx_plan_desc.flags
 # output selection bits of a group extraction (MGX_OUT_* in include/meyda_gpu.h)
 OUT_LOUDNESS_SPECIFIC, OUT_MFCC, OUT_AMPLITUDE, OUT_POWER, OUT_COMPLEX = (1 << 13, 1 << 14, 1 << 15, 1 << 16,
                                                                           1 << 17)
@@ -59,7 +60,7 @@ class PlanDesc(ctypes.Structure):
                 ("precision", ctypes.c_uint32), ("mode", ctypes.c_uint32),
                 ("num_bark_bands", ctypes.c_uint32), ("num_mel_bands", ctypes.c_uint32),
                 ("num_mfcc_coeffs", ctypes.c_uint32), ("scalar_f64", ctypes.c_uint32),
-                ("device", ctypes.c_int32)]
+                ("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
 
 
 class Outputs(ctypes.Structure):
@@ -159,7 +160,7 @@ def check(rc):
 
 def make_desc(buffer_size=512, sample_rate=44100.0, window="hanning", precision="faithful",
               mode="per_buffer_fft", num_mel_bands=26, num_mfcc_coeffs=13, scalar_f64=False,
-              device=0):
+              device=0, dct_sequential=False):
     d = PlanDesc()
     lib().mgx_plan_desc_init(ctypes.byref(d))
     d.buffer_size = buffer_size
@@ -171,6 +172,7 @@ def make_desc(buffer_size=512, sample_rate=44100.0, window="hanning", precision=
     d.num_mfcc_coeffs = num_mfcc_coeffs
     d.scalar_f64 = 1 if scalar_f64 else 0
     d.device = device
+    d.flags = FLAG_DCT_SEQUENTIAL if dct_sequential else 0
     return d
 
 

@@ -376,13 +376,16 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
     int rc = ensure(&m.xfer, &m.xfer_bytes, need, "hipMalloc(transfer buffers)");
     if (rc) return rc;
   }
-  // order after the callers' streams
+  // Extraction runs on the caller's stream (or the member's own): no cross-stream wait on
+  // the compute path. Transfers and the root's scatters run on the communication stream,
+  // ordered after what the caller enqueued before (the scatters write the root's outputs).
+  std::vector<hipStream_t> cs(g->m.size());
   for (size_t i = 0; i < g->m.size(); ++i) {
     Member& m = g->m[i];
+    cs[i] = streams && streams[i] ? static_cast<hipStream_t>(streams[i]) : m.s_comp;
+    if (R == 1) continue;
     HIP_OK(hipSetDevice(m.device), "hipSetDevice");
-    hipStream_t us = streams ? static_cast<hipStream_t>(streams[i]) : nullptr;
-    HIP_OK(hipEventRecord(m.ev_start, us), "hipEventRecord");
-    HIP_OK(hipStreamWaitEvent(m.s_comp, m.ev_start, 0), "hipStreamWaitEvent");
+    HIP_OK(hipEventRecord(m.ev_start, cs[i]), "hipEventRecord");
     HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_start, 0), "hipStreamWaitEvent");
   }
   Rccl* rc_ = R > 1 ? rccl() : nullptr;
@@ -390,25 +393,26 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
   for (uint32_t c = 0; c < nch; ++c) {
     const int sl = (int)(c & 1);
     // extraction of chunk c on every local rank
-    for (Member& m : g->m) {
+    for (size_t i = 0; i < g->m.size(); ++i) {
+      Member& m = g->m[i];
       uint64_t c0, cn;
       chunk_of(counts[m.rank], nch, c, &c0, &cn);
       HIP_OK(hipSetDevice(m.device), "hipSetDevice");
-      const float* src = frames[&m - &g->m[0]] + c0 * N;
+      const float* src = frames[i] + c0 * N;
       if (m.rank == 0) {
         if (cn) {
           const mgx_outputs o = offset_outputs(d, *root_out, mask, start[0] + c0);
-          int rc = mgx_extract_device(m.plan, src, cn, &o, m.s_comp);
+          int rc = mgx_extract_device(m.plan, src, cn, &o, cs[i]);
           if (rc) return rc;
         }
       } else {
-        if (c >= 2) HIP_OK(hipStreamWaitEvent(m.s_comp, m.ev_sent[sl], 0), "hipStreamWaitEvent");
+        if (c >= 2) HIP_OK(hipStreamWaitEvent(cs[i], m.ev_sent[sl], 0), "hipStreamWaitEvent");
         if (cn) {
           const mgx_outputs o = packed_outputs(d, m.xfer + sl * slot, mask, cn);
-          int rc = mgx_extract_device(m.plan, src, cn, &o, m.s_comp);
+          int rc = mgx_extract_device(m.plan, src, cn, &o, cs[i]);
           if (rc) return rc;
         }
-        HIP_OK(hipEventRecord(m.ev_comp[sl], m.s_comp), "hipEventRecord");
+        HIP_OK(hipEventRecord(m.ev_comp[sl], cs[i]), "hipEventRecord");
         HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_comp[sl], 0), "hipStreamWaitEvent");
       }
     }
@@ -458,15 +462,12 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
       }
     }
   }
-  // the callers' streams wait for the extraction and the gather
-  for (size_t i = 0; i < g->m.size(); ++i) {
+  // the callers' streams (or the members' own) wait for the gather
+  for (size_t i = 0; i < g->m.size() && R > 1; ++i) {
     Member& m = g->m[i];
     HIP_OK(hipSetDevice(m.device), "hipSetDevice");
-    hipStream_t us = streams ? static_cast<hipStream_t>(streams[i]) : nullptr;
-    HIP_OK(hipEventRecord(m.ev_comp_done, m.s_comp), "hipEventRecord");
     HIP_OK(hipEventRecord(m.ev_comm_done, m.s_comm), "hipEventRecord");
-    HIP_OK(hipStreamWaitEvent(us, m.ev_comp_done, 0), "hipStreamWaitEvent");
-    HIP_OK(hipStreamWaitEvent(us, m.ev_comm_done, 0), "hipStreamWaitEvent");
+    HIP_OK(hipStreamWaitEvent(cs[i], m.ev_comm_done, 0), "hipStreamWaitEvent");
   }
   return MGX_OK;
 }
@@ -526,7 +527,7 @@ int mgx_group_extract_host(mgx_group* g, const float* frames, uint64_t nframes, 
   if (rc) return rc;
   for (Member& m : g->m) {
     HIP_OK(hipSetDevice(m.device), "hipSetDevice");
-    HIP_OK(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIP_OK(hipStreamSynchronize(m.s_comp), "hipStreamSynchronize");
   }
   HIP_OK(hipSetDevice(root.device), "hipSetDevice");
   for (int i = 0; i < kFields; ++i) {

@@ -1,9 +1,9 @@
 // Fused per-frame feature extraction for gfx950 (MI355X).
 //
-// One launch processes a batch of frames. Each 256-thread workgroup loops over
-// batches of FB frames:
+// One persistent launch processes a batch of frames. Each of the 4 waves of a 256-thread
+// workgroup loops over its own batches of FPW frames:
 //
-//  Phase 1 (one wave per frame, FB/4 frames per wave, next frame prefetched):
+//  Phase 1 (one wave per frame, the next frame prefetched mid-frame):
 //    load + rms/energy/zcr      src/extractors/rms.js, energy.js, zcr.js
 //    window                     src/meyda.js:158-168
 //    FFT                        lib/jsfft/fft.js:123-208, restated as a Hermitian
@@ -12,16 +12,19 @@
 //                               N/2 complex "slots"; every stage is rounded to
 //                               float32 exactly where jsfft stores to Float32Array,
 //                               with float64 butterflies.
-//    amplitude                  src/meyda.js:104-114 -> LDS batch buffer
+//    amplitude                  src/meyda.js:104-114 -> the wave's LDS slot buffer
 //    per-frame reductions       moments (src/utils.js:1-11), log sum
 //                               (spectralFlatness.js), prefix sums (spectralRolloff.js,
 //                               loudness band sums loudness.js:47-66), DPP wave sums
-//  Phase 2 (whole workgroup, over the batch):
-//    mel filterbank             mfcc.js:40-62 as an MFMA GEMM on the matrix cores
-//                               (v_mfma_f32_16x16x4_f32: 16 bands x 16 frames per tile,
-//                               K = the bins of the tile's banded support)
+//    mel filterbank             mfcc.js:40-62 as a segmented scan over the bins (7 %
+//                               dense: no dense contraction for the matrix cores, §4.3)
+//  Phase 2 (the wave, over its FPW-frame batch):
 //    specific loudness          loudness.js:55-63 (x^0.23, float32 store)
-//    log mel + DCT              mfcc.js:64-93 (double, sequential as written)
+//    log mel + DCT              mfcc.js:64-93: the 13 x 26 DCT, the path's one dense
+//                               contraction, on the FP64 matrix cores (v_mfma_f64_4x4x4_4b:
+//                               16 coefficients x the batch's 4 frames per instruction);
+//                               MGX_FLAG_DCT_SEQUENTIAL keeps the reference's sequential
+//                               VALU order instead
 //    scalar features            spectral*.js, perceptual*.js
 //
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit.
@@ -40,23 +43,9 @@ constexpr double kS = 0.7071067811865476;  // Math.SQRT1_2 (lib/jsfft/fft.js:10)
 constexpr float kSf = 0.70710677f;
 constexpr double kLn2 = 0.6931471805599453;
 
-// Timing ablations (tools/build_abl.sh): -DMGX_ABL_NO_<PART> drops a phase-2 part.
-#define ABL_ON(part) (!MGX_ABL_NO_##part)
-#ifndef MGX_ABL_NO_LOUD2
-#define MGX_ABL_NO_LOUD2 0
-#endif
-#ifndef MGX_ABL_NO_COMB
-#define MGX_ABL_NO_COMB 0
-#endif
-#ifndef MGX_ABL_NO_DCT
-#define MGX_ABL_NO_DCT 0
-#endif
-#ifndef MGX_ABL_NO_FIN
-#define MGX_ABL_NO_FIN 0
-#endif
-#ifndef MGX_ABL_NO_MELSCAN
-#define MGX_ABL_NO_MELSCAN 0
-#endif
+// Tuning knobs (-DMGX_...) select among equivalent forms measured in DESIGN.md; every
+// setting computes the same results. Timing ablations that drop work are not in this file:
+// tools/ablate.py builds them from a patched copy.
 
 constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v >> 1); }
 constexpr int rev_bits(int x, int bits) {
@@ -117,11 +106,7 @@ struct Geo {
   // Moment sums through an LDS transpose (5 rows of 64 doubles per wave, row stride 72 so
   // the rows read together fall in different banks) rather than 5 DPP wave sums: measured
   // faster up to N = 1024 (4+ waves per SIMD), slower at 2048 (2 waves).
-#ifdef MGX_ABL_MOMDPP
-  static constexpr bool MOM_LDS = N <= 512;
-#else
   static constexpr bool MOM_LDS = N <= 1024;
-#endif
   static constexpr int MOM_STRIDE = 72;
   // Register prefetch of the next frame. A vector-memory wait is in issue order (vmcnt),
   // so a table load a frame waits on (window, twiddles) also waits for a prefetch issued
@@ -278,12 +263,6 @@ __device__ __forceinline__ void lds_barrier() {
 
 __device__ __forceinline__ double2 ld_tw_u(GTw p, int i);
 __device__ __forceinline__ double2 ld_tw(GTw p, int i) {
-#ifdef MGX_ABL_TWUNI
-  return ld_tw_u(p, __builtin_amdgcn_readfirstlane(i));  // timing ablation: scalar twiddle loads
-#endif
-#ifdef MGX_ABL_TWCONST
-  return make_double2((double)i * 1e-3, 0.7);  // timing ablation: no twiddle loads
-#endif
   const GD q = (GD)p;
   return make_double2(q[2 * i], q[2 * i + 1]);
 }
@@ -373,15 +352,10 @@ __device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf 
     const double g2 = __builtin_fma(kS, Lr, -Ar), g3 = __builtin_fma(-kS, Li, Ai);
     const double s0 = kS * (Lr + Rr), s1 = kS * (Lr - Rr);
     const double s2 = __builtin_fma(kS, Li, f.x * Ri), s3 = f.y * Ri;  // f = S f_{w/2}
-#ifdef MGX_ABL_MIXGEN
-    lo.x = (float)g0; lo.y = (float)g1; hi.x = (float)g2; hi.y = (float)g3;
-    (void)s0; (void)s1; (void)s2; (void)s3; (void)sp;
-#else
     lo.x = (float)(sp ? s0 : g0);
     lo.y = (float)(sp ? s1 : g1);
     hi.x = (float)(sp ? s2 : g2);
     hi.y = (float)(sp ? s3 : g3);
-#endif
   } else {
     const float2 c = ld_twf(twf, idx);
     const float2 f = ld_twf_u(twf, fidx);
@@ -463,7 +437,6 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
     if constexpr (P == 0) {
       if (rp == 0) bfly_special<FAITH>(v[r], v[hi], tw, twf, fidx);
       else bfly_generic<FAITH, true>(v[r], v[hi], tw, twf, mask + rp);
-#ifndef MGX_ABL_BRANCH
     } else if (rp == 0) {
       if constexpr (FAITH && TAME) {
         // every mixed pair of the stage has rp == 0: one coefficient entry per lane and stage
@@ -481,20 +454,6 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
         }
       }
       else bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, fidx, la == 0);
-#else
-    } else if (rp == 0) {
-      // Block-start on the lanes with la == 0 only: every lane runs the generic
-      // butterfly, then those lanes redo the pair as the block-start one (an exec-masked
-      // branch: cheaper than evaluating and selecting both forms on every lane).
-      const float2 lo0 = v[r], hi0 = v[hi];
-      bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + la);
-      if (la == 0) {
-        float2 a = lo0, b = hi0;
-        bfly_special<FAITH>(a, b, tw, twf, fidx);
-        v[r] = a;
-        v[hi] = b;
-      }
-#endif
     } else {
       bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + (la | rp));
     }
@@ -580,11 +539,7 @@ __device__ __forceinline__ double wave_inclusive_scan(double v) {
 // Amplitude of one slot: src/meyda.js:104-114, sqrt(re^2 + im^2) in double, stored to float32.
 template <bool FAITH>
 __device__ __forceinline__ float slot_amp(float re, float im) {
-#ifdef MGX_ABL_AMP32
-  if constexpr (false) {
-#else
   if constexpr (FAITH) {
-#endif
     // s = re^2 + im^2 lies in [2^-298, 2^256) or is 0/inf/NaN, so the library sqrt's
     // range scaling is not needed: rsq seed + the two-residual refinement (full double
     // accuracy), then 0/inf/NaN pass through.
@@ -939,13 +894,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   if (!ap->need_spectrum) return;  // (the prefetch was issued at the top: nothing to wait on)
   // Every sample finite and |x| <= 2^50 (each lane's sum of squares <= 2^100, not NaN):
   // no stage of the FFT can reach an infinity (bfly_mixed_tame).
-#if defined(MGX_ABL_NOTAME)
-  const bool tame = false;
-#elif defined(MGX_ABL_ALLTAME)
-  const bool tame = true;
-#else
   const bool tame = !__ballot(!(e32 <= 0x1p100f));
-#endif
   MGX_MARK(window);
 
   // src/meyda.js:158-168: windowed[i] = sig[i] * w[i], stored to Float32Array
@@ -989,7 +938,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     int lpf[G::NPASS];
 #pragma unroll
     for (int p = 0; p < G::NPASS; ++p) lpf[p] = G::LPREMAT ? PG::lanepart(p, opaque(lane)) : lp[p];
-#ifndef MGX_ABL_NO_PASSES
     if constexpr (FAITH) {
       // pass 0 has no mixed pairs; the later passes take the tame form when they can
       run_stages<N, 0, 0, FAITH, false>(v, lpf[0], tw, twf, twm);
@@ -999,12 +947,10 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     } else {
       run_passes<N, 0, FAITH, false>(v, lpf, buf, tw, twf, twm);
     }
-#endif
     MGX_MARK(fft_done);
     const bool want_cplx = ap->out.complex_real != nullptr;
     // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
     float ar[R];
-#ifndef MGX_ABL_AMP64
     if constexpr (FAITH) {
       bool ok = true;
 #pragma unroll
@@ -1019,9 +965,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #pragma unroll
         for (int r = 0; r < R; ++r) ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);
       }
-    } else
-#endif
-    {
+    } else {
 #pragma unroll
       for (int r = 0; r < R; ++r) ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);
     }
@@ -1077,7 +1021,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
   }
 
-#ifndef MGX_ABL_NO_REDUCE
   // Per-frame reductions, lane t owns bins [R t, R t + R).
   float av[R];
 #pragma unroll
@@ -1188,17 +1131,12 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   if (ap->need_mfcc) mt.load(ap, lane);
   prefetch_next();
   if (!kMomLds && need_mom) {
-#ifdef MGX_ABL_NOWSUM
-    const double S1 = readlane_d(P1, 63), S2 = readlane_d(P2, 63), S3 = readlane_d(P3, 63), S4 = readlane_d(P4, 63);
-    const double l2 = readlane_d((double)l2f, 63);
-#else
     const double S1 = wave_sum(P1);
     double S2 = 0, S3 = 0, S4 = 0, l2 = 0;
     if (need_hi) {
       S2 = wave_sum(P2); S3 = wave_sum(P3); S4 = wave_sum(P4);
       l2 = wave_sum((double)l2f);
     }
-#endif
     wave_sync();
     if (lane == 0) {
       rec.S[1] = S1; rec.S[2] = S2; rec.S[3] = S3; rec.S[4] = S4;
@@ -1223,7 +1161,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   MGX_MARK(bands_done);
   if (!(total < __builtin_huge_val())) {
     nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
-  } else if (ABL_ON(MELSCAN) && ap->need_mfcc) {
+  } else if (ap->need_mfcc) {
     mel_energies<N>(ap, av, lane, buf, rec, mt);
   }
   MGX_MARK(mel_done);
@@ -1237,9 +1175,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     t += dpp_d<0x141>(t);  // row_half_mirror: each 8-lane group holds its row's total
     if (lane < 40 && (lane & 7) == 0) (&rec.S[1])[row] = t;  // S[1..4], then ln2sum
   }
-#else
-  prefetch_next();  // (timing ablation: the frames are still read)
-#endif
   MGX_MARK(frame_end);
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
 }
@@ -1273,6 +1208,26 @@ __device__ __forceinline__ double exp2_mean(double y) {
   return ldexp((double)__builtin_amdgcn_exp2f((float)(y - n)), (int)n);
 }
 
+// sqrt(x) from the hardware reciprocal square root and one Newton step (relative error
+// ~1e-15) instead of the IEEE square-root sequence; 0, +inf and negative/NaN inputs give
+// sqrt's own values (0, inf, NaN).
+__device__ __forceinline__ double sqrt_d(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  const double g = x * y, h = 0.5 * y;
+  const double r = __builtin_fma(-h, g, 0.5);
+  const double s = __builtin_fma(g, r, g);
+  return (x > 0.0 && x < __builtin_huge_val()) ? s : (x == 0.0 || x == __builtin_huge_val()) ? x : __builtin_nan("");
+}
+
+// 1/x from the hardware reciprocal and one Newton step (relative error ~1e-16, against the
+// 1e-5 bar) instead of the IEEE division sequence; 0, +-inf and NaN keep the raw reciprocal's
+// IEEE values (inf, 0, NaN), where the Newton step would turn them into NaN.
+__device__ __forceinline__ double rcp_d(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  const double e = __builtin_fma(-x, r, 1.0);
+  return __builtin_fabs(e) < 1.0 ? __builtin_fma(r, e, r) : r;
+}
+
 // One of the ten spectral/time scalars of a frame from its phase-1 record, formulas as
 // written in the reference extractors. Branch-free: every lane evaluates the shared terms
 // (moments, spread) and selects its feature's numerator and denominator, so a wave
@@ -1283,9 +1238,9 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   const double S0 = rc.S[0];
   // utils.js:1-11 mu(p) = sum k^p a_k / sum a_k: one reciprocal and four products (S0 is
   // 0, >= 2^-149 or non-finite, so 1/S0 neither overflows nor hides a NaN of the quotient)
-  const double inv = 1.0 / S0;
+  const double inv = rcp_d(S0);
   const double m1 = rc.S[1] * inv, m2 = rc.S[2] * inv, m3 = rc.S[3] * inv, m4 = rc.S[4] * inv;
-  const double sd = sqrt(m2 - m1 * m1);  // spectralSpread.js
+  const double sd = sqrt_d(m2 - m1 * m1);  // spectralSpread.js
   double num, den = 1.0;
   switch (sc) {  // selects only (no divergent code: every case is a few operands)
     case MGX_RMS: num = rc.energy * (1.0 / N); break;  // rms.js: sqrt(sum / N), N a power of 2
@@ -1311,8 +1266,8 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
       den = sd * sd * sd * sd;
       break;
   }
-  const double v = num / den;
-  return sc == MGX_RMS ? sqrt(v) : v;
+  const double v = num * rcp_d(den);
+  return sc == MGX_RMS ? sqrt_d(v) : v;
 }
 
 template <int N, bool FAITH, bool LITERAL, bool SUB>
@@ -1361,10 +1316,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // frame, then phase 2 over the batch, with wave-level synchronisation only.
   const uint64_t nf = ap->num_frames;
   const uint64_t nb = (nf + FPW - 1) / FPW;
-#ifdef MGX_ABL_GRIDSTRIDE
-  const uint64_t wstride = (uint64_t)gridDim.x * 4;
-  const uint64_t b0 = (uint64_t)blockIdx.x * 4 + wave, bend = nb;
-#else
   // Each workgroup owns one contiguous range of batches, its 4 waves interleaved
   // (wave w takes batches 4k + w), so the 16 frames the waves finish together are
   // consecutive: a workgroup fills whole 64/128-byte lines of every scalar output in its
@@ -1373,7 +1324,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   const uint64_t ng = (nb + 3) / 4, per = (ng + gridDim.x - 1) / gridDim.x;
   const uint64_t g0 = (uint64_t)blockIdx.x * per, g1 = g0 + per < ng ? g0 + per : ng;
   const uint64_t b0 = g0 * 4 + wave, bend = g1 * 4 < nb ? g1 * 4 : nb;
-#endif
   // Loads are unconditional (the frame index is clamped; results of frames past the end
   // are never stored), so they issue back to back with no branches or waits between them.
   // With G::PREFETCH the next frame of the wave is loaded while this one is processed.
@@ -1415,9 +1365,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     }
     wave_sync();
 
-#ifdef MGX_ABL_NO_PHASE2
-    if (opaque(0)) {
-#endif
     // ------------------------------------------------------------- phase 2
     // Lane ids and the argument pointer are re-derived so that nothing phase 2 needs is
     // hoisted out of the batch loop (it would stay live across the FFT).
@@ -1425,7 +1372,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     {
       KArgs* q = args_ptr();
       const int l2 = opaque(lane);
-      if (ABL_ON(LOUD2) && q->need_spectrum && q->need_loudness) {
+      if (q->need_spectrum && q->need_loudness) {
         // 32 lanes per frame (24 bands + 8 idle), so a frame's reductions stay in two DPP rows.
 #pragma unroll
         for (int i0 = 0; i0 < FPW * 32; i0 += 64) {
@@ -1451,7 +1398,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
           // rows 2r and 2r+1 hold one frame: row_bcast:15 adds row 2r's total into row 2r+1
           tot += dpp_d<0x142, 0xA>(tot); mx = fmaxf(mx, dpp_f<0x142, 0xA>(mx)); sh += dpp_f<0x142, 0xA>(sh);
           if (bnd == 31 && f < q->num_frames) {
-            const double rt = 1.0 / tot;  // one division for both quotients (<= 1 ulp apart)
+            const double rt = rcp_d(tot);  // one reciprocal for both quotients
             const double ps = (tot - (double)mx) * rt;
             const double sv[3] = {tot, ps * ps, ((double)sh + q->sharp_tail_sum) * (0.11 * rt)};
 #pragma unroll
@@ -1465,7 +1412,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         }
       }
       MGX_MARK(loud2_done);
-      if (ABL_ON(COMB) && q->need_spectrum && q->need_mfcc) {
+      if (q->need_spectrum && q->need_mfcc) {
         // mfcc.js:64 Math.log of the band energies, stored to Float32Array
         const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
         for (int i = l2; i < FPW * nfp; i += 64) {
@@ -1479,57 +1426,47 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       KArgs* q = args_ptr();
       const int l2 = opaque(lane);
       MGX_MARK(ln_done);
-      if (ABL_ON(DCT) && q->need_spectrum && q->need_mfcc) {
+      if (q->need_spectrum && q->need_mfcc) {
         const int nc = q->ncoef, nfilt = q->nfilt;
-#ifndef MGX_DCT_MFMA
-        // VALU: one lane per (coefficient, frame). (The MFMA form below measured 2 % slower
-        // for the whole kernel at N = 1024: DESIGN.md §4.2.)
+        if (q->dct_sequential) {
+        // MGX_FLAG_DCT_SEQUENTIAL: VALU FMAs in the reference's sequential order, one lane per
+        // (coefficient, frame). (The matrix-core form below is the default: 0.5 % faster for the
+        // whole kernel and equal on every golden coefficient)
         for (int i = l2; i < FPW * nc; i += 64) {
           const int c = i / FPW, fb = i % FPW;
           const uint64_t f = f0 + fb;
           const double v = dct_sum(dct_lds, recs[fb].lm, c, nc, nfilt);
           if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(v / nc);
         }
-#else
-        // mfcc.js:85-93 as a dense contraction on the matrix cores: D[c][f] = sum_n
-        // dct[c][n] lm_f[n] with v_mfma_f64_16x16x4_f64 (A = DCT rows, B = the batch's
-        // log-mel columns, K = 4 bands per step). Products of two floats are exact in
-        // double, as in the reference; only the order of the f64 sum differs (~1e-16).
-        // Lane l: A[c = l & 15][k = l >> 4], B[k = l >> 4][f = l & 15];
-        // D: f = l & 15, c = (l >> 4) + 4 r (r = 0..3).
-        static_assert(FPW <= 16, "one MFMA column per frame of the batch");
-        const int col = l2 & 15, krow = l2 >> 4, ks = (nfilt + 3) >> 2;
-        const float* lmcol = recs[col < FPW ? col : 0].lm;
+        } else {
+        // mfcc.js:85-93 on the FP64 matrix cores, v_mfma_f64_4x4x4_4b_f64: 4 blocks of a
+        // 4 x 4 x 4 product per instruction. Block g holds coefficients 4g..4g+3 of a
+        // 16-coefficient tile against the batch's 4 frames; a step covers 4 bands. Lane layout
+        // (measured, tools/ubench/mfma_f64_4x4_layout.hip): A[i][k] of block g at lane
+        // 16k + 4g + i, B[k][j] at 16k + 4g + j, D[i][j] at 16i + 4g + j. So lane l loads
+        // DCT[c = l & 15][band n0 + (l >> 4)] and lm[frame l & 3][band n0 + (l >> 4)], and ends
+        // with coefficient 4 ((l >> 2) & 3) + (l >> 4) of frame l & 3. The products of two
+        // floats are exact in double, as in the reference; only the f64 summation order differs.
+        static_assert(FPW == 4, "one 4 x 4 block column per frame of the batch");
+        const int kk = l2 >> 4, fa = l2 & 3, nsteps = (nfilt + 3) >> 2;
+        const float* lmrow = recs[fa].lm;
         for (int mt = 0; mt < nc; mt += 16) {
-          typedef double f64x4 __attribute__((ext_vector_type(4)));
-          // two independent accumulation chains (even / odd steps; the tables are padded
-          // to 8 bands, so the steps come in pairs) halve the MFMA dependency latency
-          f64x4 acc = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-          const int ca = mt + col;
-          for (int st = 0; st < ks; st += 2) {
-            const int n = 4 * st + krow;  // < nfilt rounded up to 8: tables are zero-padded
-            const float av0 = ca < nc ? dct_lds[ca + n * nc] : 0.0f;
-            const float bv0 = col < FPW ? lmcol[n] : 0.0f;
-            const float av1 = ca < nc ? dct_lds[ca + (n + 4) * nc] : 0.0f;
-            const float bv1 = col < FPW ? lmcol[n + 4] : 0.0f;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)av0, (double)bv0, acc, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)av1, (double)bv1, acc1, 0, 0, 0);
+          const int ca = mt + (l2 & 15);
+          double acc = 0.0;
+          for (int st = 0; st < nsteps; ++st) {
+            const int n = 4 * st + kk;  // < nfilt rounded up to 8: the tables are zero-padded
+            const float av = ca < nc ? dct_lds[ca + n * nc] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)av, (double)lmrow[n], acc, 0, 0, 0);
           }
-          acc += acc1;
-          const uint64_t f = f0 + col;
-          if (col < FPW && f < q->num_frames && q->out.mfcc) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int c = mt + krow + 4 * r;
-              if (c < nc) gbl(q->out.mfcc)[f * nc + c] = (float)(acc[r] / nc);
-            }
-          }
+          const int c = mt + 4 * ((l2 >> 2) & 3) + kk;
+          const uint64_t f = f0 + fa;
+          if (c < nc && f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(acc / nc);
         }
-#endif
+        }
       }
       MGX_MARK(dct_done);
       // the other scalar features: one lane per (feature, frame)
-      for (int i = l2; ABL_ON(FIN) && i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {
+      for (int i = l2; i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {
         const int sc = i / FPW, fb = i % FPW;
         const uint64_t f = f0 + fb;
         void* dst = reinterpret_cast<void* const*>(smem + LY::kc_off)[sc];
@@ -1539,9 +1476,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         else gbl(static_cast<float*>(dst))[f] = (float)v;
       }
     }
-#ifdef MGX_ABL_NO_PHASE2
-    }
-#endif
     MGX_MARK(phase2_end);
     wave_sync();  // records and slot buffer are reused by the next batch
   }

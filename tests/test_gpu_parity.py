@@ -98,6 +98,24 @@ def test_mfcc_40_bands(capi, n):
 
 
 @pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("bands", [26, 40])
+def test_dct_on_matrix_cores(capi, n, bands):
+    """The default DCT (mfcc.js:85-93) runs on v_mfma_f64_4x4x4_4b_f64; MGX_FLAG_DCT_SEQUENTIAL
+    keeps the reference's sequential VALU order. The products are the same exact f32 x f32
+    products; only the f64 summation order differs, so the float32 coefficients of the two
+    match on (nearly) every element, and both match the golden outputs within the MFCC bar."""
+    g = golden_io.load(n)
+    ref = g["mfcc"] if bands == 26 else g["mfcc40"]
+    out = capi.Plan(buffer_size=n, num_mel_bands=bands).extract(g["input"], ["mfcc", "rms"])
+    assert not tolerance.check_vectors(out["mfcc"], ref)
+    base = capi.Plan(buffer_size=n, num_mel_bands=bands, dct_sequential=True).extract(g["input"], ["mfcc"])
+    assert not tolerance.check_vectors(base["mfcc"], ref)
+    same = np.mean(out["mfcc"].view(np.uint32) == base["mfcc"].view(np.uint32))
+    assert same > 0.98, same
+    print("N=%d bands=%d: DCT on MFMA equals the sequential VALU form on %.4f of the coefficients" % (n, bands, same))
+
+
+@pytest.mark.parametrize("n", SIZES)
 def test_hamming_window(capi, n):
     g = golden_io.load(n)
     idx = g["hamming_frames"]

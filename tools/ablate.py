@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Timing ablations, kept out of the product source: builds abl/libabl_<name>.so from a
+patched copy of the kernel in which one part's work is skipped (results are WRONG: for
+timing only, with MEYDA_AMD_LIB pointing at the variant). Each patch is anchored on text
+of meyda_amd/csrc/kernels.hip and fails loudly if the anchor moved.
+usage: ablate.py NAME [NAME ...]   (names: see PATCHES; 'all' builds every one)"""
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "meyda_amd", "csrc")
+
+# name -> list of (anchor, replacement); opaque(0) keeps the skipped code compiled but never run
+PATCHES = {
+    "no_phase2": [("    MGX_MARK(phase2_start);\n    {", "    MGX_MARK(phase2_start);\n    if (opaque(0)) {\n    {"),
+                  ("    MGX_MARK(phase2_end);", "    }\n    MGX_MARK(phase2_end);")],
+    "no_loud2": [("if (q->need_spectrum && q->need_loudness) {", "if (opaque(0) && q->need_spectrum && q->need_loudness) {")],
+    "no_ln": [("if (q->need_spectrum && q->need_mfcc) {\n        // mfcc.js:64",
+               "if (opaque(0) && q->need_spectrum && q->need_mfcc) {\n        // mfcc.js:64")],
+    "no_dct": [("if (q->need_spectrum && q->need_mfcc) {\n        const int nc",
+                "if (opaque(0) && q->need_spectrum && q->need_mfcc) {\n        const int nc")],
+    "no_scalars": [("for (int i = l2; i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {",
+                    "for (int i = l2; opaque(0) && i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {")],
+    "no_mel": [("  } else if (ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && ap->need_mfcc) {\n    mel_energies")],
+}
+
+
+def build(name, flags=()):
+    src = open(os.path.join(SRC, "kernels.hip")).read()
+    for old, new in PATCHES[name]:
+        if src.count(old) != 1:
+            raise SystemExit("%s: anchor found %d times: %r" % (name, src.count(old), old[:60]))
+        src = src.replace(old, new)
+    os.makedirs(os.path.join(ROOT, "abl"), exist_ok=True)
+    tmp = tempfile.NamedTemporaryFile("w", suffix=".hip", dir=SRC, prefix=".abl_", delete=False)
+    tmp.write(src)
+    tmp.close()
+    out = os.path.join(ROOT, "abl", "libabl_%s.so" % name)
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
+           "-mllvm", "-disable-machine-licm", *flags, "-shared", "-o", out, "-x", "hip", tmp.name,
+           os.path.join(SRC, "plan.cpp"), os.path.join(SRC, "group.cpp"), "-ldl"]
+    return subprocess.Popen(cmd), tmp.name, out
+
+
+def main():
+    names = sys.argv[1:] or ["all"]
+    if names == ["all"]:
+        names = list(PATCHES)
+    jobs = [build(n) for n in names]
+    rc = 0
+    for p, tmp, out in jobs:
+        rc |= p.wait()
+        os.unlink(tmp)
+        print(("built " if p.returncode == 0 else "FAILED ") + out)
+    sys.exit(rc)
+
+
+if __name__ == "__main__":
+    main()
