@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=262144, help="frames per GPU per step")
     ap.add_argument("--precision", default="faithful", choices=["faithful", "fast"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     ap.add_argument("--cpu-seconds", type=float, default=6.0,
                     help="CPU baseline: seconds of the multi-thread run (1 thread and the C port: a third)")
     ap.add_argument("--also-fast", action="store_true", help="report the fp32 mode alongside")
@@ -136,6 +137,23 @@ def settle(step, ms, dist=None):
             t = torch.tensor([1 if go else 0], dtype=torch.int32)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             go = bool(t.item())
+
+
+def host_path(plan, frames, reps=3):
+    """Secondary, never `value`: the PCIe-inclusive rate of mgx_extract_host, float32 frames in
+    pageable host memory -> every feature in host memory (chunk i+1's copy beside chunk i's
+    extraction), median of `reps` calls over the same F frames."""
+    x = frames.cpu().numpy()
+    plan.extract(x[:4096], FEATURES)  # staging allocation
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        plan.extract(x, FEATURES)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"value": x.shape[0] / t, "unit": "frames/s", "ms_per_call": t * 1e3,
+            "input_GBps": x.nbytes / t / 1e9,
+            "note": "PCIe-inclusive: %d float32 frames from pageable host memory, features back to host" % x.shape[0]}
 
 
 def run_mode(step, steps, warmup, dist):
@@ -265,6 +283,8 @@ def main():
             line["valu"] = valu
         if fast:
             line["fast_mode"] = fast
+        if world == 1 and not args.no_host_path:
+            line["host_path"] = host_path(plan, frames)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -321,13 +321,15 @@ struct mgx_plan {
   mgx::DevTables t{};
   double freq_sum = 0, pow_freq_sum = 0, nyq = 0, sharp_tail = 0;
   int grid_cap = 1;
-  // staging for mgx_extract_host
-  float* s_frames = nullptr;
-  unsigned char* s_out = nullptr;
+  // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
+  float* s_frames[2] = {nullptr, nullptr};
+  unsigned char* s_out[2] = {nullptr, nullptr};
   size_t s_out_bytes = 0;
   uint64_t s_chunk = 0;
-  unsigned char* s_pcm = nullptr;   // staging for mgx_extract_host_pcm
+  unsigned char* s_pcm[2] = {nullptr, nullptr};  // raw PCM slots for mgx_extract_host_pcm
   uint64_t s_pcm_bytes = 0;
+  hipStream_t s_copy = nullptr, s_comp = nullptr;
+  hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr}, ev_back[2] = {nullptr, nullptr};
 };
 
 extern "C" {
@@ -491,9 +493,17 @@ int mgx_plan_destroy(mgx_plan* p) {
   if (!p) return MGX_OK;
   (void)hipSetDevice(p->d.device);
   if (p->dev) (void)hipFree(p->dev);
-  if (p->s_frames) (void)hipFree(p->s_frames);
-  if (p->s_out) (void)hipFree(p->s_out);
-  if (p->s_pcm) (void)hipFree(p->s_pcm);
+  if (p->s_copy) (void)hipStreamSynchronize(p->s_copy);
+  if (p->s_comp) (void)hipStreamSynchronize(p->s_comp);
+  for (int i = 0; i < 2; ++i) {
+    if (p->s_frames[i]) (void)hipFree(p->s_frames[i]);
+    if (p->s_out[i]) (void)hipFree(p->s_out[i]);
+    if (p->s_pcm[i]) (void)hipFree(p->s_pcm[i]);
+    for (hipEvent_t ev : {p->ev_loaded[i], p->ev_done[i], p->ev_back[i]})
+      if (ev) (void)hipEventDestroy(ev);
+  }
+  if (p->s_copy) (void)hipStreamDestroy(p->s_copy);
+  if (p->s_comp) (void)hipStreamDestroy(p->s_comp);
   delete p;
   return MGX_OK;
 }
@@ -549,9 +559,44 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
 
 namespace {
 
-// Host batches: stage `nframes` frames through plan-owned device buffers in chunks.
-// `fill(f0, cnt)` puts frames [f0, f0 + cnt) into p->s_frames; outputs come back to the
-// host arrays of `o` (laid out over all nframes).
+// Host batches: `nframes` frames through two plan-owned device slots, kHostChunk frames at a
+// time. `fill(f0, cnt, slot, stream)` enqueues the copy of frames [f0, f0 + cnt) into slot
+// `slot` (p->s_frames[slot]) on the copy stream. Chunk i+1's host-to-device copy runs while
+// chunk i is extracted on the compute stream; chunk i's outputs then return to the host
+// arrays of `o` (laid out over all nframes) on the copy stream.
+int ensure_host_staging(mgx_plan* p, uint64_t chunk, size_t out_bytes) {
+  hipError_t e = hipSetDevice(p->d.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if (!p->s_copy) {
+    e = hipStreamCreateWithFlags(&p->s_copy, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->s_comp, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+      e = hipEventCreateWithFlags(&p->ev_loaded[i], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_done[i], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_back[i], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) return hip_fail(e, "host staging streams");
+  }
+  if (p->s_chunk >= chunk && p->s_out_bytes >= out_bytes) return MGX_OK;
+  for (int i = 0; i < 2; ++i) {
+    if (p->s_frames[i]) (void)hipFree(p->s_frames[i]);
+    if (p->s_out[i]) (void)hipFree(p->s_out[i]);
+    p->s_frames[i] = nullptr;
+    p->s_out[i] = nullptr;
+  }
+  p->s_chunk = 0;
+  p->s_out_bytes = 0;
+  for (int i = 0; i < 2; ++i) {
+    e = hipMalloc(reinterpret_cast<void**>(&p->s_frames[i]), chunk * p->n * sizeof(float));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging frames)");
+    e = hipMalloc(reinterpret_cast<void**>(&p->s_out[i]), out_bytes);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging outputs)");
+  }
+  p->s_chunk = chunk;
+  p->s_out_bytes = out_bytes;
+  return MGX_OK;
+}
+
 template <typename Fill>
 int extract_host_chunked(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill fill) {
   const int n = p->n, L = p->L;
@@ -563,52 +608,64 @@ int extract_host_chunked(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fi
   per += (o->loudness_specific ? nb * 4 : 0) + (o->mfcc ? nc * 4 : 0) + (o->amplitude_spectrum ? L * 4 : 0) +
          (o->power_spectrum ? L * 4 : 0) + (o->complex_real ? 2 * (size_t)n * 4 : 0);
   const uint64_t chunk = std::min<uint64_t>(nframes, kHostChunk);
-  hipError_t e = hipSetDevice(p->d.device);
-  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  if (p->s_chunk < chunk || p->s_out_bytes < per * chunk + 4096) {
-    if (p->s_frames) (void)hipFree(p->s_frames);
-    if (p->s_out) (void)hipFree(p->s_out);
-    p->s_frames = nullptr;
-    p->s_out = nullptr;
-    p->s_chunk = 0;
-    p->s_out_bytes = 0;
-    e = hipMalloc(reinterpret_cast<void**>(&p->s_frames), chunk * n * sizeof(float));
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging frames)");
-    const size_t ob = per * chunk + 4096;
-    e = hipMalloc(reinterpret_cast<void**>(&p->s_out), ob);
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging outputs)");
-    p->s_chunk = chunk;
-    p->s_out_bytes = ob;
-  }
-  for (uint64_t f0 = 0; f0 < nframes; f0 += chunk) {
-    const uint64_t cnt = std::min<uint64_t>(chunk, nframes - f0);
-    int rc = fill(f0, cnt);
-    if (rc) return rc;
+  int rc = ensure_host_staging(p, chunk, per * chunk + 4096);
+  if (rc) return rc;
+  const uint64_t nch = (nframes + chunk - 1) / chunk;
+  hipError_t e = hipSuccess;
+  auto fail_sync = [&](int code) {  // leave no work in flight on the plan's buffers
+    (void)hipStreamSynchronize(p->s_comp);
+    (void)hipStreamSynchronize(p->s_copy);
+    return code;
+  };
+  rc = fill(0, std::min<uint64_t>(chunk, nframes), 0, p->s_copy);
+  if (rc) return fail_sync(rc);
+  e = hipEventRecord(p->ev_loaded[0], p->s_copy);
+  for (uint64_t i = 0; i < nch && e == hipSuccess; ++i) {
+    const int sl = (int)(i & 1);
+    const uint64_t f0 = i * chunk, cnt = std::min<uint64_t>(chunk, nframes - f0);
     mgx_outputs d{};
     size_t off = 0;
-    auto take = [&](size_t bytes) { unsigned char* q = p->s_out + off; off += (bytes + 255) / 256 * 256; return q; };
-    for (int i = 0; i < MGX_NUM_SCALARS; ++i) d.scalars[i] = o->scalars[i] ? take(cnt * ss) : nullptr;
+    auto take = [&](size_t bytes) { unsigned char* q = p->s_out[sl] + off; off += (bytes + 255) / 256 * 256; return q; };
+    for (int k = 0; k < MGX_NUM_SCALARS; ++k) d.scalars[k] = o->scalars[k] ? take(cnt * ss) : nullptr;
     d.loudness_specific = o->loudness_specific ? reinterpret_cast<float*>(take(cnt * nb * 4)) : nullptr;
     d.mfcc = o->mfcc ? reinterpret_cast<float*>(take(cnt * nc * 4)) : nullptr;
     d.amplitude_spectrum = o->amplitude_spectrum ? reinterpret_cast<float*>(take(cnt * L * 4)) : nullptr;
     d.power_spectrum = o->power_spectrum ? reinterpret_cast<float*>(take(cnt * L * 4)) : nullptr;
     d.complex_real = o->complex_real ? reinterpret_cast<float*>(take(cnt * n * 4)) : nullptr;
     d.complex_imag = o->complex_imag ? reinterpret_cast<float*>(take(cnt * n * 4)) : nullptr;
-    rc = mgx_extract_device(p, p->s_frames, cnt, &d, nullptr);
-    if (rc) return rc;
+    // extraction of chunk i: after its frames arrived and chunk i-2's outputs left the slot
+    e = hipStreamWaitEvent(p->s_comp, p->ev_loaded[sl], 0);
+    if (e == hipSuccess && i >= 2) e = hipStreamWaitEvent(p->s_comp, p->ev_back[sl], 0);
+    if (e != hipSuccess) break;
+    rc = mgx_extract_device(p, p->s_frames[sl], cnt, &d, p->s_comp);
+    if (rc) return fail_sync(rc);
+    e = hipEventRecord(p->ev_done[sl], p->s_comp);
+    // chunk i+1's frames into the other slot once chunk i-1's extraction has read them
+    if (e == hipSuccess && i + 1 < nch) {
+      const uint64_t g0 = (i + 1) * chunk, gc = std::min<uint64_t>(chunk, nframes - g0);
+      if (i >= 1) e = hipStreamWaitEvent(p->s_copy, p->ev_done[sl ^ 1], 0);
+      if (e != hipSuccess) break;
+      rc = fill(g0, gc, sl ^ 1, p->s_copy);
+      if (rc) return fail_sync(rc);
+      e = hipEventRecord(p->ev_loaded[sl ^ 1], p->s_copy);
+    }
+    // chunk i's outputs back to the caller's arrays
+    if (e == hipSuccess) e = hipStreamWaitEvent(p->s_copy, p->ev_done[sl], 0);
     auto back = [&](void* host, const void* dev, size_t bytes) {
-      return host ? hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost) : hipSuccess;
+      return host ? hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, p->s_copy) : hipSuccess;
     };
-    for (int i = 0; i < MGX_NUM_SCALARS && e == hipSuccess; ++i)
-      if (o->scalars[i]) e = back(static_cast<unsigned char*>(o->scalars[i]) + f0 * ss, d.scalars[i], cnt * ss);
+    for (int k = 0; k < MGX_NUM_SCALARS && e == hipSuccess; ++k)
+      if (o->scalars[k]) e = back(static_cast<unsigned char*>(o->scalars[k]) + f0 * ss, d.scalars[k], cnt * ss);
     if (e == hipSuccess && o->loudness_specific) e = back(o->loudness_specific + f0 * nb, d.loudness_specific, cnt * nb * 4);
     if (e == hipSuccess && o->mfcc) e = back(o->mfcc + f0 * nc, d.mfcc, cnt * nc * 4);
     if (e == hipSuccess && o->amplitude_spectrum) e = back(o->amplitude_spectrum + f0 * L, d.amplitude_spectrum, cnt * L * 4);
     if (e == hipSuccess && o->power_spectrum) e = back(o->power_spectrum + f0 * L, d.power_spectrum, cnt * L * 4);
     if (e == hipSuccess && o->complex_real) e = back(o->complex_real + f0 * n, d.complex_real, cnt * n * 4);
     if (e == hipSuccess && o->complex_imag) e = back(o->complex_imag + f0 * n, d.complex_imag, cnt * n * 4);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(outputs)");
+    if (e == hipSuccess) e = hipEventRecord(p->ev_back[sl], p->s_copy);
   }
+  if (e == hipSuccess) e = hipStreamSynchronize(p->s_copy);
+  if (e != hipSuccess) return fail_sync(hip_fail(e, "host batch copies"));
   return MGX_OK;
 }
 
@@ -637,9 +694,9 @@ int mgx_extract_host(mgx_plan* p, const float* frames, uint64_t nframes, const m
   if ((o->complex_real == nullptr) != (o->complex_imag == nullptr))
     return fail(MGX_E_INVALID_ARGUMENT, "complex_real and complex_imag must be given together");
   const int n = p->n;
-  return extract_host_chunked(p, nframes, o, [&](uint64_t f0, uint64_t cnt) {
-    hipError_t e = hipMemcpy(p->s_frames, frames + f0 * n, cnt * n * sizeof(float), hipMemcpyHostToDevice);
-    return e == hipSuccess ? MGX_OK : hip_fail(e, "hipMemcpy(frames)");
+  return extract_host_chunked(p, nframes, o, [&](uint64_t f0, uint64_t cnt, int slot, hipStream_t st) {
+    hipError_t e = hipMemcpyAsync(p->s_frames[slot], frames + f0 * n, cnt * n * sizeof(float), hipMemcpyHostToDevice, st);
+    return e == hipSuccess ? MGX_OK : hip_fail(e, "hipMemcpyAsync(frames)");
   });
 }
 
@@ -726,20 +783,23 @@ int mgx_extract_host_pcm(mgx_plan* p, const void* pcm, uint64_t pcm_bytes, uint6
                 (unsigned long long)sample_frames, (unsigned long long)align, (unsigned long long)pcm_bytes);
   const uint64_t chunk_bytes = std::min<uint64_t>(nframes, kHostChunk) * n * align;
   if (p->s_pcm_bytes < chunk_bytes) {
-    if (p->s_pcm) (void)hipFree(p->s_pcm);
-    p->s_pcm = nullptr;
+    if (p->s_copy) (void)hipStreamSynchronize(p->s_copy);
+    for (int i = 0; i < 2; ++i) {
+      if (p->s_pcm[i]) (void)hipFree(p->s_pcm[i]);
+      p->s_pcm[i] = nullptr;
+    }
     p->s_pcm_bytes = 0;
     hipError_t e = hipSetDevice(p->d.device);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p->s_pcm), chunk_bytes);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipMalloc(reinterpret_cast<void**>(&p->s_pcm[i]), chunk_bytes);
     if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging PCM)");
     p->s_pcm_bytes = chunk_bytes;
   }
   const unsigned char* src = static_cast<const unsigned char*>(pcm);
-  return extract_host_chunked(p, nframes, o, [&](uint64_t f0, uint64_t cnt) {
+  return extract_host_chunked(p, nframes, o, [&](uint64_t f0, uint64_t cnt, int slot, hipStream_t st) {
     const uint64_t bytes = cnt * n * align;
-    hipError_t e = hipMemcpy(p->s_pcm, src + f0 * n * align, bytes, hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(pcm)");
-    e = mgx::launch_pcm_decode(p->s_pcm, cnt * n, format, channels, channel, p->s_frames, nullptr);
+    hipError_t e = hipMemcpyAsync(p->s_pcm[slot], src + f0 * n * align, bytes, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(pcm)");
+    e = mgx::launch_pcm_decode(p->s_pcm[slot], cnt * n, format, channels, channel, p->s_frames[slot], st);
     return e == hipSuccess ? MGX_OK : hip_fail(e, "PCM decode launch");
   });
 }
