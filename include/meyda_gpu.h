@@ -120,6 +120,12 @@ typedef struct mgx_plan_desc {
 #define MGX_FLAG_DCT_SEQUENTIAL 1u  /* mfcc.js:85-93 DCT as VALU FMAs in the reference's sequential
                                         order instead of the FP64 matrix cores (the default: same
                                         exact products, f64 sums in 4-band blocks) */
+#define MGX_FLAG_MFCC_REFERENCE 2u  /* mfcc.js:53-93 in the reference's own order: each mel band summed
+                                        over its bins in ascending order into a float32 accumulator of
+                                        double products, Math.log in double, the sequential DCT (MFCC
+                                        bit-identical wherever the power spectrum is; slower, see
+                                        DESIGN.md §4.3). Default off: segmented-scan mel sums, float32
+                                        hardware log, the matrix-core DCT, all within 1e-5. */
 
 typedef struct mgx_plan mgx_plan;
 

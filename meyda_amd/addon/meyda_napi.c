@@ -134,6 +134,7 @@ static int desc_from_opts(napi_env env, napi_value opts, mgx_plan_desc* d) {
   if (get_u32_prop(env, opts, "device", &u)) d->device = (int32_t)u;
   if (get_u32_prop(env, opts, "scalarF64", &u)) d->scalar_f64 = u ? 1 : 0;
   if (get_u32_prop(env, opts, "dctSequential", &u) && u) d->flags |= MGX_FLAG_DCT_SEQUENTIAL;
+  if (get_u32_prop(env, opts, "mfccReferenceOrder", &u) && u) d->flags |= MGX_FLAG_MFCC_REFERENCE;
   return 1;
 }
 

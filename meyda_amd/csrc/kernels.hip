@@ -807,6 +807,57 @@ __device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av
   }
 }
 
+// MGX_FLAG_MFCC_REFERENCE: the mel band energies in the reference's own order (mfcc.js:40-62).
+// Lane j < nfilt owns band j and walks its bins in ascending order: the weight
+// (k - b_j) / (b_{j+1} - b_j) on the rising segment, (b_{j+2} - k) / (b_{j+2} - b_{j+1}) on the
+// falling one, each the correctly rounded double quotient; the product with the float32 power
+// rounded to double; the sum rounded to double and stored to the Float32Array accumulator.
+// Bins outside [b_j, b_{j+2}) carry weight 0 in the reference and add exactly +0 there (finite
+// frames only; non-finite ones take nonfinite_frame_sums). The quotient t/d of two small
+// integers comes from r = 1/d (IEEE, once per segment) as q0 = t r, e = t - q0 d (exact by
+// FMA), q0 + e r: the correctly rounded quotient for every 0 <= t <= d <= 4096 (checked
+// exhaustively on the CPU; tests/test_capi_host.py), with no division in the loop.
+template <int N>
+__device__ __forceinline__ void mel_reference_order(KArgs* ap, const float (&av)[Geo<N>::R], int lane, float2* buf,
+                                                    FrameRec& rec) {
+  constexpr int R = Geo<N>::R;
+  double* prow = reinterpret_cast<double*>(buf);  // the frame's power spectrum, float32 values in double
+  wave_sync();  // band-sum reads of the prefix buffer are done
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) prow[R * lane + jj] = (double)(av[jj] * av[jj]);  // powerSpectrum.js
+  wave_sync();
+  const int nf = ap->nfilt;
+  if (lane < nf) {
+    const auto b = gbl(ap->t.mel_bins);
+    constexpr int L = N / 2;  // the reference sums bins j < N/2 only
+    const int b0 = min(b[lane], L), b1 = min(b[lane + 1], L), b2 = min(b[lane + 2], L);
+    double acc = 0.0;  // the Float32Array element, held exactly in double
+    // One segment, 4 bins per step: the weights and products of a step are independent, only
+    // the accumulator is serial. Bins past the segment's end contribute an exact +0 (their
+    // product is selected away, never multiplied: the slot buffer holds other data there).
+    auto segment = [&](int k0, int k1, bool rising) {
+      if (k1 <= k0) return;
+      const double d = (double)(k1 - k0), r = 1.0 / d;
+      for (int k = k0; k < k1; k += 4) {
+        double pr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double t = (double)(rising ? k + u - k0 : k1 - k - u);
+          const double q0 = t * r;
+          const double w = __builtin_fma(__builtin_fma(-q0, d, t), r, q0);
+          const double p = prow[k + u];
+          pr[u] = k + u < k1 ? w * p : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = (double)(float)(acc + pr[u]);  // two double roundings, the float32 store
+      }
+    };
+    segment(b0, b1, true);
+    segment(b1, b2, false);
+    rec.lm[lane] = (float)acc;
+  }
+}
+
 // One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
 template <int N, bool FAITH, bool LITERAL, bool SUB>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
@@ -1161,6 +1212,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   MGX_MARK(bands_done);
   if (!(total < __builtin_huge_val())) {
     nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
+  } else if (SUB && ap->need_mfcc && ap->mfcc_reference) {  // (the all-feature kernel never has the flag)
+    mel_reference_order<N>(ap, av, lane, buf, rec);
   } else if (ap->need_mfcc) {
     mel_energies<N>(ap, av, lane, buf, rec, mt);
   }
@@ -1415,9 +1468,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       if (q->need_spectrum && q->need_mfcc) {
         // mfcc.js:64 Math.log of the band energies, stored to Float32Array
         const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
+        const bool ref_log = SUB && q->mfcc_reference;  // the double Math.log, then float32
         for (int i = l2; i < FPW * nfp; i += 64) {
           const int band = i / FPW, fb = i % FPW;
-          recs[fb].lm[band] = band < nfilt ? ln_f32(recs[fb].lm[band]) : 0.0f;  // padding for dct_sum
+          recs[fb].lm[band] = band < nfilt ? (ref_log ? (float)log((double)recs[fb].lm[band]) : ln_f32(recs[fb].lm[band]))
+                                           : 0.0f;  // padding for dct_sum
         }
       }
     }
@@ -1428,7 +1483,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       MGX_MARK(ln_done);
       if (q->need_spectrum && q->need_mfcc) {
         const int nc = q->ncoef, nfilt = q->nfilt;
-        if (q->dct_sequential) {
+        if (q->dct_sequential || (SUB && q->mfcc_reference)) {
         // MGX_FLAG_DCT_SEQUENTIAL: VALU FMAs in the reference's sequential order, one lane per
         // (coefficient, frame). (The matrix-core form below is the default: 0.5 % faster for the
         // whole kernel and equal on every golden coefficient)
@@ -1569,7 +1624,9 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
   if (mode == MGX_MODE_LITERAL) return launch_n<N, true, true>(a, grid, stream);
   if (precision == MGX_PRECISION_FAST) return launch_n<N, false, false>(a, grid, stream);
   // a spectral feature subset that skips the moment / prefix work takes the SUB kernel
-  if (a.need_spectrum && !(a.need_mom == 2 && a.need_prefix)) return launch_n<N, true, false, true>(a, grid, stream);
+  // (and so does MGX_FLAG_MFCC_REFERENCE: the all-feature kernel keeps its schedule)
+  if (a.need_spectrum && (!(a.need_mom == 2 && a.need_prefix) || a.mfcc_reference))
+    return launch_n<N, true, false, true>(a, grid, stream);
   return launch_n<N, true, false>(a, grid, stream);
 }
 

@@ -47,6 +47,7 @@ struct KernelArgs {
   int need_mom;          // 2: flatness / spread / skewness / kurtosis (S1..S4, sum log2 a); 1: centroid / slope (S1); 0
   int need_prefix;       // rolloff or loudness: the prefix row (rolloff count, bark band sums)
   int dct_sequential;    // MGX_FLAG_DCT_SEQUENTIAL: the DCT as VALU FMAs in the reference's order
+  int mfcc_reference;    // MGX_FLAG_MFCC_REFERENCE: mel sums, log and DCT in the reference's order (SUB kernel)
 };
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.

@@ -300,7 +300,7 @@ int validate(const mgx_plan_desc* d) {
     return fail(MGX_E_UNSUPPORTED, "num_mel_bands must be in [1, %d]", mgx::kMaxMel);
   if (d->num_mfcc_coeffs < 1 || d->num_mfcc_coeffs > (uint32_t)mgx::kMaxCoeffs)
     return fail(MGX_E_UNSUPPORTED, "num_mfcc_coeffs must be in [1, %d]", mgx::kMaxCoeffs);
-  if (d->flags & ~MGX_FLAG_DCT_SEQUENTIAL) return fail(MGX_E_INVALID_ARGUMENT, "unknown plan flags 0x%x", d->flags);
+  if (d->flags & ~(MGX_FLAG_DCT_SEQUENTIAL | MGX_FLAG_MFCC_REFERENCE)) return fail(MGX_E_INVALID_ARGUMENT, "unknown plan flags 0x%x", d->flags);
   return MGX_OK;
 }
 
@@ -534,6 +534,7 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.ncoef = (int)p->d.num_mfcc_coeffs;
   a.scalar_f64 = (int)p->d.scalar_f64;
   a.dct_sequential = (p->d.flags & MGX_FLAG_DCT_SEQUENTIAL) ? 1 : 0;
+  a.mfcc_reference = (p->d.flags & MGX_FLAG_MFCC_REFERENCE) ? 1 : 0;
   bool spec = o->loudness_specific || o->mfcc || o->amplitude_spectrum || o->power_spectrum || o->complex_real;
   for (int i = MGX_SPECTRAL_CENTROID; i < MGX_NUM_SCALARS; ++i) spec = spec || o->scalars[i];
   a.need_spectrum = spec;

@@ -107,6 +107,8 @@ class Meyda {
       precision: this.options.precision, mode: this.options.mode,
       numMelBands: this.options.numMelBands, numMfccCoeffs: this.options.numMfccCoeffs,
       device: this.options.device, scalarF64: 1,
+      // options.mfccReferenceOrder: mel sums, log and DCT in mfcc.js's own order (bit-identical MFCC)
+      mfccReferenceOrder: this.options.mfccReferenceOrder ? 1 : 0,
       // options.devices = [d0, d1, ...]: every batch is sharded over the devices and the
       // per-frame features are gathered to d0 over xGMI (RCCL), include/meyda_gpu.h mgx_group_*
       ...(Array.isArray(this.options.devices) ? { devices: this.options.devices } : {}),

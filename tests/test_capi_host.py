@@ -112,3 +112,34 @@ def test_host_tables_tiny_buffer_sizes(capi, n):
     if L == 0:
         assert np.all(t["bark_limits"][:-1] == 0)
     assert t["hanning"].shape == (n,) and t["bark_scale"].shape == (n,)
+
+
+def test_mel_weight_division_is_correctly_rounded(tmp_path):
+    """kernels.hip mel_reference_order: the weight t/d of two small integers comes from
+    r = 1/d as q0 = t r, e = fma(-q0, d, t), fma(e, r, q0). Exhaustively equal to the IEEE
+    quotient (what mfcc.js:44-50 computes) for every 0 <= t <= d <= 4096."""
+    import shutil
+    import subprocess
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    src = tmp_path / "div.c"
+    src.write_text(r"""
+#include <math.h>
+#include <stdio.h>
+int main(void) {
+  long bad = 0;
+  for (int d = 1; d <= 4096; ++d) {
+    volatile double dd = d, r = 1.0 / dd;
+    for (int t = 0; t <= d; ++t) {
+      volatile double tt = t, ref = tt / dd;
+      const double q0 = tt * r;
+      if (fma(fma(-q0, dd, tt), r, q0) != ref) ++bad;
+    }
+  }
+  printf("%ld\n", bad);
+  return 0;
+}
+""")
+    exe = tmp_path / "div"
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(src), "-lm"])
+    assert subprocess.check_output([str(exe)]).decode().strip() == "0"
