@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: time the shards alone, without the RCCL gather to rank 0")
     ap.add_argument("--chunks", type=int, default=0, help="N > 1: gather pipeline depth (0 = automatic)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="N = 1: skip the live rocprofv3 --pmc passes (HBM traffic, VALU instruction mix)")
     return ap.parse_args()
 
 
@@ -156,6 +158,55 @@ def host_path(plan, frames, reps=3):
             "note": "PCIe-inclusive: %d float32 frames from pageable host memory, features back to host" % x.shape[0]}
 
 
+def pmc_live(n, F, precision):
+    """Counters of the same workload, measured in this run: rocprofv3 --pmc passes (one
+    counter block each, kernel-trace only, MI355X_MICROARCH.md HBM section) over
+    tools/pmc_probe.py in a child process. FETCH_SIZE is calibrated on the time-only feature
+    set, which reads exactly the frames (gfx950 tallies streaming reads at about half their
+    bytes); WRITE_SIZE is read as is. Returns (traffic bytes per launch, VALU mix, notes)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, None, "rocprofv3 not found"
+    probe = os.path.join(ROOT, "tools", "pmc_probe.py")
+    tmp = tempfile.mkdtemp(prefix="mgx_pmc_", dir="/tmp")
+    passes = {"fetch_t": ("time_only", "FETCH_SIZE"), "fetch": ("all", "FETCH_SIZE"), "write": ("all", "WRITE_SIZE"),
+              "valu": ("all", "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 "
+                              "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS")}
+    got = {}
+    for key, (fset, ctrs) in passes.items():
+        d = os.path.join(tmp, key)
+        env = dict(os.environ, PROBE_SET=fset, PROBE_N=str(n), PROBE_PREC=precision, PROBE_REPS="3", TMPDIR="/tmp")
+        cmd = ["timeout", "-s", "KILL", "90", prof, "--pmc", *ctrs.split(), "--kernel-trace", "--output-format", "csv",
+               "-d", d, "-o", "run", "--", sys.executable, probe]
+        r = subprocess.run(cmd, env=env, cwd="/tmp", capture_output=True, text=True)
+        if r.returncode != 0:
+            return None, None, "rocprofv3 pass %s failed (rc %d)" % (key, r.returncode)
+        vals = {}
+        for f in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                if "extract_kernel" in row.get("Kernel_Name", ""):
+                    vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+        got[key] = {k: float(np.mean(v)) for k, v in vals.items()}
+    shutil.rmtree(tmp, ignore_errors=True)
+    frames_bytes = F * n * 4
+    cal = frames_bytes / (got["fetch_t"]["FETCH_SIZE"] * 1024)  # true bytes per counted byte (KB counters)
+    read = got["fetch"]["FETCH_SIZE"] * 1024 * cal
+    write = got["write"]["WRITE_SIZE"] * 1024
+    v = got["valu"]
+    valu = {"instr_per_frame": v["SQ_INSTS_VALU"] / F, "cvt_per_frame": v["SQ_INSTS_VALU_CVT"] / F,
+            "f64_per_frame": sum(v[k] for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
+                                                "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")) / F,
+            "lds_per_frame": v["SQ_INSTS_LDS"] / F}
+    note = ("live: rocprofv3 --pmc passes of this run over tools/pmc_probe.py (%d frames x N=%d, same features); "
+            "FETCH_SIZE x %.4f (time-only calibration), reads %.4g B + writes %.4g B per launch" % (F, n, cal, read, write))
+    return read + write, valu, note
+
+
 def run_mode(step, steps, warmup, dist):
     """W untimed steps, then exactly `steps` timed ones bracketed by a barrier and a device
     synchronisation on both sides; HIP events on the launch stream around each step."""
@@ -234,26 +285,19 @@ def main():
     if rank == 0:
         bytes_per_frame = 4 * n + 4 * OUT_FLOATS
         achieved = F * bytes_per_frame / (kernel_ms * 1e-3) / 1e9
-        traffic = None
-        key = "%s_n%d_f%d" % (args.precision, n, F)
-        prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(prof):
-            with open(prof) as fh:
-                pj = json.load(fh)
-            if key in pj:
-                traffic = pj[key]["hbm_bytes_per_launch"]
-        # the faithful path is FP64-VALU bound; its instruction mix from the
-        # committed PMC passes (tools/gpu_pmc_cur.sh + tools/pmc_valu_json.py)
-        valu = None
-        prof = os.path.join(ROOT, "profiles", "pmc_valu.json")
-        if os.path.exists(prof):
-            with open(prof) as fh:
-                pv = json.load(fh)
-            if key in pv:
-                v = pv[key]
-                valu = {"instr_per_frame": v["valu_instr_per_frame"], "f64_per_frame": v["f64_instr_per_frame"],
-                        "cvt_per_frame": v["cvt_instr_per_frame"], "est_valu_busy": v["est_valu_busy"],
-                        "est_fp64_cvt_busy": v["est_fp64_pipe_busy"], "source": "profiles/pmc_valu.json"}
+        traffic, valu, traffic_note = None, None, "not measured (--no-pmc or N > 1)"
+        if world == 1 and not args.no_pmc:
+            try:
+                traffic, valu, traffic_note = pmc_live(n, F, args.precision)
+            except Exception as e:  # the counters are a report, never the measurement itself
+                traffic, valu, traffic_note = None, None, "rocprofv3 passes failed: %r" % (e,)
+        if valu is not None:
+            # the faithful path is FP64-VALU bound. Issue costs per wave64
+            # instruction measured by tools/ubench/op_rates.hip (profiles/r01_op_rates.log):
+            # f64 ~5.0, f32<->f64 conversion 4.2 cycles; at the clock this run's kernel time implies
+            cyc = kernel_ms * 1e-3 * 2.4e9 * 1024 / F  # SIMD cycles per frame (2.4 GHz held, 1,024 SIMDs)
+            valu["frame_simd_cycles"] = cyc
+            valu["est_fp64_cvt_busy"] = (valu["f64_per_frame"] * 5.0 + valu["cvt_per_frame"] * 4.2) / cyc
         line = {
             "metric": "audio frames/sec (bufferSize=1024, all features) at 1/2/4/8 GPUs; % HBM roofline",
             "value": world * F * args.steps / elapsed,
@@ -275,7 +319,7 @@ def main():
                        "gather": ("RCCL send/recv to rank 0 in the timed step, %s chunks" % (args.chunks or "auto"))
                        if gather else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                          "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
                          "bytes_per_frame": bytes_per_frame},
         }

@@ -23,6 +23,20 @@ PATCHES = {
                 "if (opaque(0) && q->need_spectrum && q->need_mfcc) {\n        const int nc")],
     "no_scalars": [("for (int i = l2; i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {",
                     "for (int i = l2; opaque(0) && i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {")],
+    # the frame samples from the address instead of HBM (is the frame load's latency exposed?)
+    "no_frame_load": [("""#else
+  return *p;
+#endif
+}""", """#else
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  return (float)((a >> 2) & 1023) * 0x1p-10f - 0.5f;
+#endif
+}""")],
+    # the per-lane twiddle loads of passes >= 1 made lane-uniform scalar loads
+    "twuni": [("""__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
+  const GD q = (GD)p;""", """__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
+  return ld_tw_u(p, __builtin_amdgcn_readfirstlane(i));
+  const GD q = (GD)p;""")],
     "no_mel": [("  } else if (ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && ap->need_mfcc) {\n    mel_energies")],
 }
 

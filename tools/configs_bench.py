@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Every BASELINE.json config on one GPU (informational; bench.py is the contract line).
 
-C2: 65,536 x N=512, amplitudeSpectrum + spectralCentroid
+C2: 65,536 x N=512, amplitudeSpectrum + spectralCentroid (C2-2GiB: 1,048,576 frames, beyond the MALL)
 C3: 262,144 x N=1024, spectral* + loudness (+ perceptual)
 C4: 262,144 x N=1024, 40-band mel + 13-coefficient MFCC
 C5: 262,144 x N=2048 per GPU (the 8-GPU config's shard), all features incl. MFCC
@@ -22,6 +22,9 @@ SPECTRAL = ["spectralCentroid", "spectralFlatness", "spectralSlope", "spectralRo
             "spectralSkewness", "spectralKurtosis"]
 CONFIGS = {
     "C2": dict(n=512, F=65536, feats=["amplitudeSpectrum", "spectralCentroid"], out_floats=256 + 1, mel=26),
+    # C2 again with a batch 8x the 256 MiB MALL (2 GiB of frames): the 128 MiB C2 batch stays
+    # resident in the MALL between launches, so only this row is an HBM fraction
+    "C2-2GiB": dict(n=512, F=1048576, feats=["amplitudeSpectrum", "spectralCentroid"], out_floats=256 + 1, mel=26),
     "C3": dict(n=1024, F=262144, feats=SPECTRAL + ["loudness", "perceptualSpread", "perceptualSharpness"],
                out_floats=7 + 25 + 2, mel=26),
     "C4": dict(n=1024, F=262144, feats=["mfcc"], out_floats=13, mel=40),
