@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: time the shards alone, without the RCCL gather to rank 0")
     ap.add_argument("--chunks", type=int, default=0, help="N > 1: gather pipeline depth (0 = automatic)")
+    ap.add_argument("--no-every-output", action="store_true",
+                    help="N = 1: skip the secondary timing with every output (spectra too) and 40 mel bands")
     ap.add_argument("--no-pmc", action="store_true",
                     help="N = 1: skip the live rocprofv3 --pmc passes (HBM traffic, VALU instruction mix)")
     return ap.parse_args()
@@ -282,6 +284,23 @@ def main():
         el_f, km_f = run_mode(step_f, args.steps, args.warmup, dist)
         fast = {"value": world * F * args.steps / el_f, "kernel_ms": km_f,
                 "roofline_frac": (F * (4 * n + 4 * OUT_FLOATS)) / (km_f * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    every = None
+    if world == 1 and not args.no_every_output:
+        # Secondary (never `value`): EVERY output of the path — the headline set plus the
+        # amplitude, power and complex spectra — with the 40-band mel of config C4, same frames
+        plan_e = capi.Plan(buffer_size=n, precision=args.precision, num_mel_bands=40, device=dev)
+        feats_e = FEATURES + ["amplitudeSpectrum", "powerSpectrum", "complexSpectrum"]
+        outs_e, o_e = plan_e.alloc_outputs(F, feats_e)
+
+        def step_e(s):
+            plan_e.extract_device(frames.data_ptr(), F, o_e, s)
+        settle(step_e, args.settle_ms)
+        el_e, km_e = run_mode(step_e, args.steps, args.warmup, dist)
+        bpf_e = 4 * n + 4 * (OUT_FLOATS + 2 * (n // 2) + 2 * n)
+        every = {"features": feats_e, "mel_bands": 40, "value": F * args.steps / el_e, "unit": "frames/s",
+                 "kernel_ms": km_e, "bytes_per_frame": bpf_e,
+                 "roofline_frac": F * bpf_e / (km_e * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        del outs_e, o_e
     if rank == 0:
         bytes_per_frame = 4 * n + 4 * OUT_FLOATS
         achieved = F * bytes_per_frame / (kernel_ms * 1e-3) / 1e9
@@ -327,6 +346,8 @@ def main():
             line["valu"] = valu
         if fast:
             line["fast_mode"] = fast
+        if every:
+            line["every_output"] = every
         if world == 1 and not args.no_host_path:
             line["host_path"] = host_path(plan, frames)
         if not args.no_cpu_baseline and world == 1:

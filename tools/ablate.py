@@ -37,6 +37,11 @@ PATCHES = {
   const GD q = (GD)p;""", """__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
   return ld_tw_u(p, __builtin_amdgcn_readfirstlane(i));
   const GD q = (GD)p;""")],
+    # the window table loads (16 per frame at N = 1024) replaced by a constant
+    "no_window_load": [("    for (int c = 0; c < CH; ++c) wv[c] = w[c * 64 + lane];",
+                        "    for (int c = 0; c < CH; ++c) wv[c] = 0.5f + 0.25f * (c & 1);")],
+    # (not an ablation: the DPP wave sums instead of the LDS transpose for the moments at N = 1024)
+    "mom_dpp": [("static constexpr bool MOM_LDS = N <= 1024;", "static constexpr bool MOM_LDS = N <= 512;")],
     "no_mel": [("  } else if (ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && ap->need_mfcc) {\n    mel_energies")],
 }
 
