@@ -41,6 +41,21 @@ check('C1: get([rms, spectralCentroid]) on sound1 frame 0', () => {
   m.dispose();
 });
 
+check('mfccReferenceOrder: the reference MFCC bits on noise frames (bit-exact spectra)', () => {
+  const m = new Meyda(ctx, null, 512, null, { mfccReferenceOrder: true });
+  let frames = 0;
+  for (let i = 0; i < g.F; i++) {
+    if (!g.labels[i].startsWith('noise')) continue;
+    m.process(frameOf(g, i));
+    const r = m.get('mfcc');
+    const ref = g.mfcc.subarray(i * 13, i * 13 + 13);
+    for (let c = 0; c < 13; c++) assert.ok(Object.is(r[c], ref[c]), g.labels[i] + ' mfcc[' + c + ']: ' + r[c] + ' vs ' + ref[c]);
+    frames++;
+  }
+  assert.ok(frames > 0);
+  m.dispose();
+});
+
 check('per-buffer get() vs reference on noise and wav frames', () => {
   const m = new Meyda(ctx, null, 512);
   let frames = 0;
