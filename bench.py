@@ -229,12 +229,20 @@ def run_mode(step, steps, warmup, dist):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    per_step = [a.elapsed_time(b) for a, b in ev]
+    kernel_ms = float(np.mean(per_step))
+    stats = {"mean_ms": kernel_ms, "median_ms": float(np.median(per_step)), "min_ms": float(np.min(per_step)),
+             "max_ms": float(np.max(per_step))}
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, kernel_ms
+        # per-GPU step times reported separately (HIP events on each rank's stream)
+        allr = [None] * dist.get_world_size()
+        dist.all_gather_object(allr, stats)
+        stats = {"rank0": stats, "per_rank_mean_ms": [r["mean_ms"] for r in allr],
+                 "per_rank_median_ms": [r["median_ms"] for r in allr]}
+    return elapsed, kernel_ms, stats
 
 
 def main():
@@ -242,7 +250,8 @@ def main():
     from meyda_amd import dist as mdist
     rank, local, world = mdist.env_rank_world()
     dist = None
-    torch.cuda.set_device(local)
+    # one GPU per rank; (a box with fewer GPUs than ranks, a rehearsal only, shares them)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
         import torch.distributed as tdist
         mdist.init("gloo")  # control plane only; the data path is the library's RCCL gather
@@ -273,7 +282,7 @@ def main():
             plan.extract_device(frames.data_ptr(), F, o, s)
     torch.cuda.synchronize()
     settle(step, args.settle_ms, dist)
-    elapsed, kernel_ms = run_mode(step, args.steps, args.warmup, dist)
+    elapsed, kernel_ms, step_stats = run_mode(step, args.steps, args.warmup, dist)
     fast = None
     if args.also_fast and args.precision != "fast" and world == 1:
         plan_f = capi.Plan(buffer_size=n, precision="fast", device=dev)
@@ -281,7 +290,7 @@ def main():
         def step_f(s):
             plan_f.extract_device(frames.data_ptr(), F, o, s)
         settle(step_f, args.settle_ms)
-        el_f, km_f = run_mode(step_f, args.steps, args.warmup, dist)
+        el_f, km_f, _ = run_mode(step_f, args.steps, args.warmup, dist)
         fast = {"value": world * F * args.steps / el_f, "kernel_ms": km_f,
                 "roofline_frac": (F * (4 * n + 4 * OUT_FLOATS)) / (km_f * 1e-3) / 1e9 / HBM_PEAK_GBS}
     every = None
@@ -295,7 +304,7 @@ def main():
         def step_e(s):
             plan_e.extract_device(frames.data_ptr(), F, o_e, s)
         settle(step_e, args.settle_ms)
-        el_e, km_e = run_mode(step_e, args.steps, args.warmup, dist)
+        el_e, km_e, _ = run_mode(step_e, args.steps, args.warmup, dist)
         bpf_e = 4 * n + 4 * (OUT_FLOATS + 2 * (n // 2) + 2 * n)
         every = {"features": feats_e, "mel_bands": 40, "value": F * args.steps / el_e, "unit": "frames/s",
                  "kernel_ms": km_e, "bytes_per_frame": bpf_e,
@@ -340,6 +349,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                          "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
+                         "step_event_ms": step_stats,
                          "bytes_per_frame": bytes_per_frame},
         }
         if valu:
