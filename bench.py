@@ -178,7 +178,9 @@ def pmc_live(n, F, precision):
     tmp = tempfile.mkdtemp(prefix="mgx_pmc_", dir="/tmp")
     passes = {"fetch_t": ("time_only", "FETCH_SIZE"), "fetch": ("all", "FETCH_SIZE"), "write": ("all", "WRITE_SIZE"),
               "valu": ("all", "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 "
-                              "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS")}
+                              "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS"),
+              "mfma": ("all", "SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES "
+                              "GRBM_GUI_ACTIVE")}
     got = {}
     for key, (fset, ctrs) in passes.items():
         d = os.path.join(tmp, key)
@@ -204,6 +206,10 @@ def pmc_live(n, F, precision):
             "f64_per_frame": sum(v[k] for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
                                                 "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")) / F,
             "lds_per_frame": v["SQ_INSTS_LDS"] / F}
+    mm = got["mfma"]
+    # the DCT's v_mfma_f64_4x4x4_4b_f64: 4 blocks x 4x4x4 = 256 FMAs = 512 FLOP per wave instruction
+    valu["mfma_f64"] = {"instr_per_launch": mm["SQ_INSTS_VALU_MFMA_F64"], "flop_per_launch": 512 * mm["SQ_INSTS_VALU_MFMA_F64"],
+                        "busy_cycles_per_launch": mm["SQ_VALU_MFMA_BUSY_CYCLES"], "gui_active_cycles": mm["GRBM_GUI_ACTIVE"]}
     note = ("live: rocprofv3 --pmc passes of this run over tools/pmc_probe.py (%d frames x N=%d, same features); "
             "FETCH_SIZE x %.4f (time-only calibration), reads %.4g B + writes %.4g B per launch" % (F, n, cal, read, write))
     return read + write, valu, note
@@ -326,6 +332,12 @@ def main():
             cyc = kernel_ms * 1e-3 * 2.4e9 * 1024 / F  # SIMD cycles per frame (2.4 GHz held, 1,024 SIMDs)
             valu["frame_simd_cycles"] = cyc
             valu["est_fp64_cvt_busy"] = (valu["f64_per_frame"] * 5.0 + valu["cvt_per_frame"] * 4.2) / cyc
+            # FP64 pipe (vector and matrix share it): 78.6 TFLOP/s dense on MI355X (1,024 SIMDs x 32
+            # FLOP/clk x 2.4 GHz; v_mfma_f64_4x4x4 issues every 16 cycles: tools/ubench/op_rates.hip)
+            mf = valu["mfma_f64"]
+            mf["tflops"] = mf["flop_per_launch"] / (kernel_ms * 1e-3) / 1e12
+            mf["peak_tflops"] = 78.6
+            mf["frac"] = mf["tflops"] / mf["peak_tflops"]
         line = {
             "metric": "audio frames/sec (bufferSize=1024, all features) at 1/2/4/8 GPUs; % HBM roofline",
             "value": world * F * args.steps / elapsed,
