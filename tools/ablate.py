@@ -42,6 +42,12 @@ PATCHES = {
                         "    for (int c = 0; c < CH; ++c) wv[c] = 0.5f + 0.25f * (c & 1);")],
     # (not an ablation: the DPP wave sums instead of the LDS transpose for the moments at N = 1024)
     "mom_dpp": [("static constexpr bool MOM_LDS = N <= 1024;", "static constexpr bool MOM_LDS = N <= 512;")],
+    # the amplitude as |re| + |im| (no f64 squares, no rsq/Heron step)
+    "no_amp": [("        ar[r] = slot_amp_rsq(v[r].x, v[r].y, okr);",
+                "        ar[r] = fabsf(v[r].x) + fabsf(v[r].y); okr = true;")],
+    # the prefix row (stores, rolloff ballots) skipped: band sums read stale LDS
+    "no_prefix": [("  const bool need_prefix = SUB ? (bool)ap->need_prefix : true;",
+                   "  const bool need_prefix = opaque(0);")],
     "no_mel": [("  } else if (ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && ap->need_mfcc) {\n    mel_energies")],
 }
 
