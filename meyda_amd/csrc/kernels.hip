@@ -106,8 +106,24 @@ struct Geo {
   // Moment sums through an LDS transpose (5 rows of 64 doubles per wave, row stride 72 so
   // the rows read together fall in different banks) rather than 5 DPP wave sums: measured
   // faster up to N = 1024 (4+ waves per SIMD), slower at 2048 (2 waves).
-  static constexpr bool MOM_LDS = N <= 1024;
+#ifndef MGX_MOM_LDS_MAXN
+#define MGX_MOM_LDS_MAXN 1024
+#endif
+  static constexpr bool MOM_LDS = N <= MGX_MOM_LDS_MAXN;
   static constexpr int MOM_STRIDE = 72;
+  // MOM_SLOT: the moment transpose runs in the wave's slot buffer right after the partials are
+  // written (one more LDS round trip, no table of its own: 11.5 KB less LDS per workgroup)
+#ifndef MGX_MOM_SLOT
+#define MGX_MOM_SLOT 1
+#endif
+  static constexpr bool MOM_SLOT = MOM_LDS && MGX_MOM_SLOT && SLOT_PHYS >= 5 * MOM_STRIDE;
+  // TW_LDS (N = 1024): the per-lane twiddles of passes >= 1 (the mixed-table entries and the
+  // generic twiddles the tame passes read) are staged in LDS once per workgroup, in the space
+  // the moment table left: LDS reads (lgkmcnt) instead of vector loads (vmcnt) in the passes
+#ifndef MGX_TW_LDS
+#define MGX_TW_LDS 1
+#endif
+  static constexpr bool TW_LDS = MGX_TW_LDS && N == 1024 && MOM_SLOT;
   // Register prefetch of the next frame. A vector-memory wait is in issue order (vmcnt),
   // so a table load a frame waits on (window, twiddles) also waits for a prefetch issued
   // before it: prefetching at the start of the frame made every frame wait for the next
@@ -169,6 +185,28 @@ struct PassGeo {
   }
 };
 
+
+// LDS image of the tame passes' per-lane twiddles (Geo<N>::TW_LDS), in double2 entries. In
+// pass P >= 1 at N = 1024 the location bits below the pass are lane bits [0, q0) and the
+// stage bits below stage q are register bits [q0, q): the mixed pairs of stage q read entries
+// mask + la, la < 2^q0 (two double2 each: (b, c0), (t4, kL)), the generic ones mask + (la | rp),
+// rp != 0, i.e. [mask + 2^q0, mask + 2^q). Per (P, I): the mixed block, then the generic one.
+template <int N>
+struct TwLds {
+  using PG = PassGeo<N>;
+  static constexpr int mixed_n(int P) { return 2 << PG::q0(P); }
+  static constexpr int gen_n(int P, int I) { return (1 << (PG::q0(P) + I)) - (1 << PG::q0(P)); }
+  static constexpr int off(int P, int I, bool gen) {
+    int o = 0;
+    for (int p = 1; p < Geo<N>::NPASS; ++p)
+      for (int i = 0; i < PG::m(p); ++i) {
+        if (p == P && i == I) return gen ? o + mixed_n(p) : o;
+        o += mixed_n(p) + gen_n(p, i);
+      }
+    return o;
+  }
+  static constexpr int total() { return off(Geo<N>::NPASS, 0, false); }
+};
 
 // Bank-padded layouts of the amplitude row (floats) and of its prefix sums (doubles) in
 // the slot buffer: lane l reads the row (ds_read2_b64) and writes the prefix
@@ -315,6 +353,17 @@ __device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, GTw tw, GTw
   }
 }
 
+// The faithful generic pair with its twiddle already in registers (TwLds).
+__device__ __forceinline__ void bfly_generic_c(float2& lo, float2& hi, double2 c) {
+  const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+  const double Ar = __builtin_fma(c.x, Rr, -(c.y * Ri));
+  const double Ai = __builtin_fma(c.x, Ri, c.y * Rr);
+  lo.x = (float)__builtin_fma(kS, Lr, Ar);
+  lo.y = (float)__builtin_fma(kS, Li, Ai);
+  hi.x = (float)__builtin_fma(kS, Lr, -Ar);
+  hi.y = (float)__builtin_fma(-kS, Li, Ai);
+}
+
 template <bool FAITH>
 __device__ __forceinline__ void bfly_special(float2& lo, float2& hi, GTw tw, GTwf twf, int idx) {
   // f = SQRT1_2 f_{w/2}: S (Lh + f_x Rh) as S Lh + (S f_x) Rh and S (f_y Rh) as (S f_y) Rh
@@ -422,7 +471,9 @@ __device__ __forceinline__ void bfly_mixed_tame(float2& lo, float2& hi, double2 
 
 // One radix-2 stage on location bit q = q0(P) + I, entirely in registers.
 template <int N, int P, int I, bool FAITH, bool TAME>
-__device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm) {
+__device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm,
+                                          const double2* twl) {
+  constexpr bool LT = FAITH && TAME && Geo<N>::TW_LDS && P > 0;  // twiddles from the LDS image
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int q = PG::q0(P) + I;
@@ -443,17 +494,20 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
         constexpr int npairs = G::R >> (I + 1);
         const bool sp = la == 0;
         const double2 fw = ld_tw_u(twm, 2 * fidx);
-        const double2 m = ld_tw(twm, 2 * (mask + la));
+        const double2 m = LT ? twl[TwLds<N>::off(P, I, false) + 2 * la] : ld_tw(twm, 2 * (mask + la));
         if constexpr (G::MIX == 0 || (G::MIX == 2 && npairs == 1)) {
           bfly_mixed_tame1(v[r], v[hi], m, fw, sp);
         } else if constexpr (G::MIX == 1) {
-          bfly_mixed_tame(v[r], v[hi], m, ld_tw(twm, 2 * (mask + la) + 1), fw.x, sp);
+          bfly_mixed_tame(v[r], v[hi], m, LT ? twl[TwLds<N>::off(P, I, false) + 2 * la + 1] : ld_tw(twm, 2 * (mask + la) + 1),
+                          fw.x, sp);
         } else {
           const double2 k = make_double2(sp ? fw.y : kS * m.x, sp ? 0.0 : -kS);
           bfly_mixed_tame(v[r], v[hi], m, k, fw.x, sp);
         }
       }
       else bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, fidx, la == 0);
+    } else if constexpr (LT) {
+      bfly_generic_c(v[r], v[hi], twl[TwLds<N>::off(P, I, true) + ((la | rp) - (1 << PassGeo<N>::q0(P)))]);
     } else {
       bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + (la | rp));
     }
@@ -461,10 +515,11 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
 }
 
 template <int N, int P, int I, bool FAITH, bool TAME>
-__device__ __forceinline__ void run_stages(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm) {
+__device__ __forceinline__ void run_stages(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm,
+                                           const double2* twl) {
   if constexpr (I < PassGeo<N>::m(P)) {
-    run_stage<N, P, I, FAITH, TAME>(v, lp, tw, twf, twm);
-    run_stages<N, P, I + 1, FAITH, TAME>(v, lp, tw, twf, twm);
+    run_stage<N, P, I, FAITH, TAME>(v, lp, tw, twf, twm, twl);
+    run_stages<N, P, I + 1, FAITH, TAME>(v, lp, tw, twf, twm, twl);
   }
 }
 
@@ -488,11 +543,11 @@ __device__ __forceinline__ void exchange(float2 (&v)[Geo<N>::R], int lp_prev, in
 
 template <int N, int P, bool FAITH, bool TAME>
 __device__ __forceinline__ void run_passes(float2 (&v)[Geo<N>::R], const int (&lp)[Geo<N>::NPASS],
-                                           float2* buf, GTw tw, GTwf twf, GTw twm) {
+                                           float2* buf, GTw tw, GTwf twf, GTw twm, const double2* twl) {
   if constexpr (P < Geo<N>::NPASS) {
     if constexpr (P > 0) exchange<N, P>(v, lp[P - 1], lp[P], buf);
-    run_stages<N, P, 0, FAITH, TAME>(v, lp[P], tw, twf, twm);
-    run_passes<N, P + 1, FAITH, TAME>(v, lp, buf, tw, twf, twm);
+    run_stages<N, P, 0, FAITH, TAME>(v, lp[P], tw, twf, twm, twl);
+    run_passes<N, P + 1, FAITH, TAME>(v, lp, buf, tw, twf, twm, twl);
   }
 }
 
@@ -662,7 +717,8 @@ struct Lds {
   static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2 + 64) * 4, "mel scratch must fit");
   // Per wave, the 5 x 64 table of moment partials (transposed reduction, N <= 512).
   static constexpr size_t mom_off = slot_off + slot_bytes;
-  static constexpr size_t mom_bytes = G::MOM_LDS ? (size_t)4 * 5 * G::MOM_STRIDE * 8 : 0;
+  static constexpr size_t mom_bytes = (G::MOM_LDS && !G::MOM_SLOT) ? (size_t)4 * 5 * G::MOM_STRIDE * 8 : 0;
+  static_assert(!G::MOM_SLOT || (size_t)G::SLOT_PHYS >= (size_t)5 * G::MOM_STRIDE, "moment table must fit the slot buffer");
   // Frame records: FPW per wave.
   static constexpr size_t rec_off = mom_off + mom_bytes;
   // Kernel constants read per lane, staged once per workgroup: the 13 scalar output
@@ -671,8 +727,12 @@ struct Lds {
   // also wait for every output store and frame load issued before it.
   static constexpr size_t kc_off = rec_off + (size_t)G::FB * sizeof(FrameRec);
   static constexpr size_t kc_bytes = 16 * 8 + 32 * 4;
+  // The tame passes' per-lane twiddles (Geo<N>::TW_LDS, TwLds), staged once per workgroup.
+  static constexpr size_t twl_off = kc_off + kc_bytes;
+  static constexpr size_t twl_bytes = G::TW_LDS ? (size_t)TwLds<N>::total() * 16 : 0;
+  static_assert(twl_off % 16 == 0, "double2 alignment");
   // The DCT table (mfcc.js:67-83), staged once per workgroup, sized per plan.
-  static constexpr size_t dct_off = kc_off + kc_bytes;
+  static constexpr size_t dct_off = twl_off + twl_bytes;
   static size_t bytes(int ncoef, int nfilt) { return dct_off + (size_t)ncoef * ((nfilt + 7) & ~7) * 4; }
 };
 
@@ -864,7 +924,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
                                              int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
                                              const int* klim, float (&xn)[Geo<N>::PREFETCH ? Geo<N>::CH : 1],
-                                             GF next) {
+                                             GF next, const double2* twl) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
@@ -1000,12 +1060,12 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     for (int p = 0; p < G::NPASS; ++p) lpf[p] = G::LPREMAT ? PG::lanepart(p, opaque(lane)) : lp[p];
     if constexpr (FAITH) {
       // pass 0 has no mixed pairs; the later passes take the tame form when they can
-      run_stages<N, 0, 0, FAITH, false>(v, lpf[0], tw, twf, twm);
+      run_stages<N, 0, 0, FAITH, false>(v, lpf[0], tw, twf, twm, twl);
       MGX_MARK(pass0_done);
-      if (tame) run_passes<N, 1, FAITH, true>(v, lpf, buf, tw, twf, twm);
-      else run_passes<N, 1, FAITH, false>(v, lpf, buf, tw, twf, twm);
+      if (tame) run_passes<N, 1, FAITH, true>(v, lpf, buf, tw, twf, twm, twl);
+      else run_passes<N, 1, FAITH, false>(v, lpf, buf, tw, twf, twm, twl);
     } else {
-      run_passes<N, 0, FAITH, false>(v, lpf, buf, tw, twf, twm);
+      run_passes<N, 0, FAITH, false>(v, lpf, buf, tw, twf, twm, twl);
     }
     MGX_MARK(fft_done);
     const bool want_cplx = ap->out.complex_real != nullptr;
@@ -1154,19 +1214,35 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   } else {
     P1 = __builtin_fma(bb, T0, P1);
   }
+  double* const momt = G::MOM_SLOT ? pbuf : mom;
   if (kMomLds && need_mom) {
-    mom[0 * MS + lane] = P1;
+    momt[0 * MS + lane] = P1;
     if (need_hi) {
-      mom[1 * MS + lane] = P2;
-      mom[2 * MS + lane] = P3;
-      mom[3 * MS + lane] = P4;
-      mom[4 * MS + lane] = (double)l2f;
+      momt[1 * MS + lane] = P2;
+      momt[2 * MS + lane] = P3;
+      momt[3 * MS + lane] = P4;
+      momt[4 * MS + lane] = (double)l2f;
     }
   }
   // prefix P(k) = sum_{i<k} a_i: lane-exclusive offset + local prefix
   const double incl = wave_inclusive_scan(T0);
   const double excl = dpp_d<0x138>(incl);  // wave_shr:1 (lane 0 reads 0)
   const double total = readlane_d(incl, 63);
+  // the moment transpose's reduction (lanes 0..39: 8 entries of one row, then 3 DPP steps)
+  auto mom_reduce = [&]() {
+    const int row = lane < 40 ? lane >> 3 : 0;
+    const double* src = momt + row * MS + (lane & 7);  // entries g, g+8, ..., g+56 of the row
+    double t = ((src[0] + src[8]) + (src[16] + src[24])) + ((src[32] + src[40]) + (src[48] + src[56]));
+    t += dpp_d<0xB1>(t);   // quad_perm [1,0,3,2]
+    t += dpp_d<0x4E>(t);   // quad_perm [2,3,0,1]
+    t += dpp_d<0x141>(t);  // row_half_mirror: each 8-lane group holds its row's total
+    if (lane < 40 && (lane & 7) == 0) (&rec.S[1])[row] = t;  // S[1..4], then ln2sum
+  };
+  if (G::MOM_SLOT && need_mom) {
+    wave_sync();
+    mom_reduce();
+    wave_sync();  // the table's reads are done: the buffer takes the prefix row
+  }
   // spectralRolloff.js:6-15: the largest m with P(m) <= 0.99 total (P(0) = 0).
   const double thr = 0.99 * total;
   int cnt = 0;
@@ -1227,15 +1303,9 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     mel_energies<N>(ap, av, lane, buf, rec, mt);
   }
   MGX_MARK(mel_done);
-  if (kMomLds && need_mom) {
+  if (kMomLds && !G::MOM_SLOT && need_mom) {
     wave_sync();
-    const int row = lane < 40 ? lane >> 3 : 0;
-    const double* src = mom + row * MS + (lane & 7);  // entries g, g+8, ..., g+56 of the row
-    double t = ((src[0] + src[8]) + (src[16] + src[24])) + ((src[32] + src[40]) + (src[48] + src[56]));
-    t += dpp_d<0xB1>(t);   // quad_perm [1,0,3,2]
-    t += dpp_d<0x4E>(t);   // quad_perm [2,3,0,1]
-    t += dpp_d<0x141>(t);  // row_half_mirror: each 8-lane group holds its row's total
-    if (lane < 40 && (lane & 7) == 0) (&rec.S[1])[row] = t;  // S[1..4], then ln2sum
+    mom_reduce();
   }
   MGX_MARK(frame_end);
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
@@ -1341,7 +1411,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
   float* dct_lds = reinterpret_cast<float*>(smem + LY::dct_off);
-  double* mom = reinterpret_cast<double*>(smem + LY::mom_off) + (threadIdx.x >> 6) * (5 * G::MOM_STRIDE);
+  double* mom = G::MOM_SLOT ? nullptr : reinterpret_cast<double*>(smem + LY::mom_off) + (threadIdx.x >> 6) * (5 * G::MOM_STRIDE);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1355,6 +1425,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     int* klim = reinterpret_cast<int*>(smem + LY::kc_off + 16 * 8);
     if (threadIdx.x < MGX_NUM_SCALARS) kptr[threadIdx.x] = ap->out.scalars[threadIdx.x];
     if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = gbl(ap->t.bblim)[threadIdx.x - 64];
+  }
+  if constexpr (G::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
+    double2* twl = reinterpret_cast<double2*>(smem + LY::twl_off);
+    const GTw tw = gbl(ap->t.tw), twm = gbl(ap->t.twm);
+    auto stage_copy = [&](auto P_, auto I_) {
+      constexpr int P = decltype(P_)::value, I = decltype(I_)::value;
+      constexpr int q0 = PG::q0(P), mask = (1 << (q0 + I)) - 1;
+      for (int i = threadIdx.x; i < TwLds<N>::mixed_n(P); i += kThreads)
+        twl[TwLds<N>::off(P, I, false) + i] = ld_tw(twm, 2 * mask + i);  // entries mask + la, la < 2^q0
+      for (int i = threadIdx.x; i < TwLds<N>::gen_n(P, I); i += kThreads)
+        twl[TwLds<N>::off(P, I, true) + i] = ld_tw(tw, mask + (1 << q0) + i);
+    };
+    static_assert(G::NPASS == 3 && PG::m(1) == 3 && PG::m(2) == 3, "TwLds: the N = 1024 pass structure");
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    using C2 = std::integral_constant<int, 2>;
+    stage_copy(C1{}, C0{}); stage_copy(C1{}, C1{}); stage_copy(C1{}, C2{});
+    stage_copy(C2{}, C0{}); stage_copy(C2{}, C1{}); stage_copy(C2{}, C2{});
   }
   if (ap->need_spectrum && ap->need_mfcc) {
     const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
@@ -1423,7 +1511,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         load(x, b, j);
       }
       frame_phase1<N, FAITH, LITERAL, SUB>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
-                                      reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next);
+                                      reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
+                                      reinterpret_cast<const double2*>(smem + LY::twl_off));
     }
     wave_sync();
 

@@ -41,7 +41,7 @@ PATCHES = {
     "no_window_load": [("    for (int c = 0; c < CH; ++c) wv[c] = w[c * 64 + lane];",
                         "    for (int c = 0; c < CH; ++c) wv[c] = 0.5f + 0.25f * (c & 1);")],
     # (not an ablation: the DPP wave sums instead of the LDS transpose for the moments at N = 1024)
-    "mom_dpp": [("static constexpr bool MOM_LDS = N <= 1024;", "static constexpr bool MOM_LDS = N <= 512;")],
+    "mom_dpp": [("#define MGX_MOM_LDS_MAXN 1024", "#define MGX_MOM_LDS_MAXN 512")],
     # the amplitude as |re| + |im| (no f64 squares, no rsq/Heron step)
     "no_amp": [("        ar[r] = slot_amp_rsq(v[r].x, v[r].y, okr);",
                 "        ar[r] = fabsf(v[r].x) + fabsf(v[r].y); okr = true;")],
