@@ -136,8 +136,19 @@ struct Geo {
 #ifdef MGX_PF_ALL
   static constexpr int PF = MGX_PF_ALL;
 #else
-  static constexpr int PF = N <= 256 ? 1 : N <= 1024 ? 2 : 0;  // measured best per N
+#ifndef MGX_PF1024
+#define MGX_PF1024 2
 #endif
+  static constexpr int PF = N <= 256 ? 1 : N < 1024 ? 2 : N == 1024 ? MGX_PF1024 : 0;  // measured best per N
+#endif
+  // WIN_REG: the window held in registers for the whole launch (CH VGPRs) instead of loaded
+  // per frame (N = 1024, where the LDS twiddles freed the registers: 1.1-1.5 % faster, 119
+  // VGPRs; the frame prefetch at the frame's start instead, MGX_PF1024=1, 0.9-1.1 %, and both
+  // together 1.1 %)
+#ifndef MGX_WIN_REG
+#define MGX_WIN_REG 1
+#endif
+  static constexpr bool WIN_REG = MGX_WIN_REG && N == 1024;
   static constexpr bool PREFETCH = PF != 0;
 #ifdef MGX_LPREMAT
   static constexpr bool LPREMAT = MGX_LPREMAT;
@@ -924,7 +935,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
                                              int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
                                              const int* klim, float (&xn)[Geo<N>::PREFETCH ? Geo<N>::CH : 1],
-                                             GF next, const double2* twl) {
+                                             GF next, const double2* twl, const float (&wreg)[Geo<N>::CH]) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
@@ -945,7 +956,10 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // faster at N = 512, equal at 1024 and 2048; a lane-major table read as 16-byte loads was
   // 2-5 % slower at 512 and 2048).
   float wv[CH];
-  if (ap->need_spectrum) {
+  if (G::WIN_REG) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) wv[c] = wreg[c];
+  } else if (ap->need_spectrum) {
     const GF w = gbl(ap->t.window);
 #pragma unroll
     for (int c = 0; c < CH; ++c) wv[c] = w[c * 64 + lane];
@@ -1488,6 +1502,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     for (int c = 0; c < CH; ++c) xv[c] = ld_frame(xin + c * 64);
   };
 
+  float wreg[CH];
+  if constexpr (G::WIN_REG) {
+    const GF w = gbl(ap->t.window);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) wreg[c] = w[c * 64 + lane];
+  }
   float xn[G::PREFETCH ? CH : 1];
   if constexpr (G::PREFETCH) load(xn, b0, 0);
 
@@ -1512,7 +1532,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       }
       frame_phase1<N, FAITH, LITERAL, SUB>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
                                       reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
-                                      reinterpret_cast<const double2*>(smem + LY::twl_off));
+                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg);
     }
     wave_sync();
 
