@@ -216,7 +216,18 @@ struct TwLds {
       }
     return o;
   }
-  static constexpr int total() { return off(Geo<N>::NPASS, 0, false); }
+  // after the per-stage blocks: the lane-uniform (f_x, S f_y) of each tame stage's block-start
+  // pair (the mixed table's entry N/2 - 1 + q), one double2 per stage q = q0(P) + I
+  static constexpr int fw_off(int P, int I) {
+    int o = off(Geo<N>::NPASS, 0, false);
+    for (int p = 1; p < Geo<N>::NPASS; ++p)
+      for (int i = 0; i < PG::m(p); ++i) {
+        if (p == P && i == I) return o;
+        ++o;
+      }
+    return o;
+  }
+  static constexpr int total() { return fw_off(Geo<N>::NPASS, 0); }
 };
 
 // Bank-padded layouts of the amplitude row (floats) and of its prefix sums (doubles) in
@@ -504,7 +515,7 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
         // every mixed pair of the stage has rp == 0: one coefficient entry per lane and stage
         constexpr int npairs = G::R >> (I + 1);
         const bool sp = la == 0;
-        const double2 fw = ld_tw_u(twm, 2 * fidx);
+        const double2 fw = LT ? twl[TwLds<N>::fw_off(P, I)] : ld_tw_u(twm, 2 * fidx);
         const double2 m = LT ? twl[TwLds<N>::off(P, I, false) + 2 * la] : ld_tw(twm, 2 * (mask + la));
         if constexpr (G::MIX == 0 || (G::MIX == 2 && npairs == 1)) {
           bfly_mixed_tame1(v[r], v[hi], m, fw, sp);
@@ -1450,6 +1461,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         twl[TwLds<N>::off(P, I, false) + i] = ld_tw(twm, 2 * mask + i);  // entries mask + la, la < 2^q0
       for (int i = threadIdx.x; i < TwLds<N>::gen_n(P, I); i += kThreads)
         twl[TwLds<N>::off(P, I, true) + i] = ld_tw(tw, mask + (1 << q0) + i);
+      if (threadIdx.x == 0) twl[TwLds<N>::fw_off(P, I)] = ld_tw(twm, 2 * (G::L - 1 + q0 + I));
     };
     static_assert(G::NPASS == 3 && PG::m(1) == 3 && PG::m(2) == 3, "TwLds: the N = 1024 pass structure");
     using C0 = std::integral_constant<int, 0>;
