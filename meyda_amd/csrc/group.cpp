@@ -359,9 +359,13 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
   }
   for (size_t i = 0; i < g->m.size(); ++i)
     if (counts[g->m[i].rank] && !frames[i]) return fail(MGX_E_INVALID_ARGUMENT, "frames of local rank %zu are NULL", i);
-  // pipeline depth: about 64 Ki frames per chunk, at most 8 chunks
-  if (nch == 0) nch = (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, (most + 65535) / 65536));
-  if (R == 1) nch = std::max<uint32_t>(nch, 1);
+  // pipeline depth: about 32 Ki frames per chunk, at most 8 chunks. Each peer's
+  // records cross one xGMI link to the root (200 B per frame: ~52 MB per 262,144-frame shard,
+  // of the order of the shard's extraction time), so what is not overlapped is about one
+  // chunk's transfer after the last extraction: 8 chunks halve that tail against 4 for ~1 % of
+  // kernel-boundary cost per extra chunk (one-rank group).
+  // (a one-rank group has nothing to overlap: one chunk)
+  if (nch == 0) nch = R == 1 ? 1 : (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, (most + 32767) / 32768));
   uint64_t cmax = 0;
   for (uint32_t r = 0; r < R; ++r) {
     uint64_t c0, cn;
