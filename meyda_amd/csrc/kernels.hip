@@ -244,16 +244,25 @@ __device__ __forceinline__ int pa_inv(int k) { return k - 4 * (k / 68); }  // pa
 __device__ __forceinline__ int pd(int d) { return d + (d >> 4); }
 
 
-// Wave priority around LDS round trips (s_setprio): a wave that reaches an exchange issues
-// its writes and reads ahead of the other waves' VALU work, so its LDS latency overlaps
-// their arithmetic. MGX_PRIOSET selects the regions: bit 0 the FFT exchanges (measured
-// 0.5-1 % faster at N = 512..2048), bit 1 also the amplitude row (no further gain).
+// Wave priority (s_setprio) in the frame's low-ILP sections: a wave in an LDS round trip or a
+// serial chain (DPP reductions, the amplitude's conversions, phase 2's scalar steps) issues
+// ahead of the other waves, whose FFT passes have independent butterflies to fill the gaps,
+// so its latency overlaps their arithmetic instead of adding to it. MGX_PRIOSET selects the
+// regions: 1 the FFT exchanges, 2 the amplitude row's LDS round trip, 4 phase 2, 8 the
+// per-frame reductions (moment transpose, prefix and rolloff, band sums, mel scan), 16 the
+// frame start (energy/zcr, window, stage 0), 32 the amplitude, 64 the moment partials.
+// Measured (interleaved A/B, all features): 1 alone 0.5-1 % faster than none;
+// 111 (all but the frame start) another 5.0 % at N = 1024, 4.3 % at 2048, 7.4 % at 512;
+// adding 16 cost N = 512 its fifth wave per SIMD (+7 %).
 #ifndef MGX_PRIOSET
-#define MGX_PRIOSET 1
+#define MGX_PRIOSET 111
+#endif
+#ifndef MGX_PRIO_P2
+#define MGX_PRIO_P2 2
 #endif
 template <int REGION>
 __device__ __forceinline__ void prio_hi() {
-  if constexpr ((MGX_PRIOSET & REGION) != 0) __builtin_amdgcn_s_setprio(2);
+  if constexpr ((MGX_PRIOSET & REGION) != 0) __builtin_amdgcn_s_setprio(REGION == 4 ? MGX_PRIO_P2 : 2);
 }
 template <int REGION>
 __device__ __forceinline__ void prio_lo() {
@@ -976,6 +985,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     for (int c = 0; c < CH; ++c) wv[c] = w[c * 64 + lane];
   }
   MGX_MARK(energy_zcr);
+  prio_hi<16>();
   // rms.js / energy.js: sum of squares; zcr.js: sign changes of adjacent samples,
   // `x >= 0` vs `x < 0` (so -0 is non-negative and NaN never counts).
   // Sum of squares as packed float32 FMAs over pairs of chunks; zcr from one ballot per
@@ -1037,7 +1047,10 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     recs[fb].energy = e;
     recs[fb].zcr = z;
   }
-  if (!ap->need_spectrum) return;  // (the prefetch was issued at the top: nothing to wait on)
+  if (!ap->need_spectrum) {  // (the prefetch was issued at the top: nothing to wait on)
+    prio_lo<16>();
+    return;
+  }
   // Every sample finite and |x| <= 2^50 (each lane's sum of squares <= 2^100, not NaN):
   // no stage of the FFT can reach an infinity (bfly_mixed_tame).
   const bool tame = !__ballot(!(e32 <= 0x1p100f));
@@ -1073,6 +1086,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
         v[r].y = kSf * (x[c] - x[c + R]);
       }
     }
+    prio_lo<16>();
     MGX_MARK(stage0_done);
     GTw tw = gbl(ap->t.tw);
     GTwf twf = gbl(ap->t.twf);
@@ -1093,6 +1107,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       run_passes<N, 0, FAITH, false>(v, lpf, buf, tw, twf, twm, twl);
     }
     MGX_MARK(fft_done);
+    prio_hi<32>();
     const bool want_cplx = ap->out.complex_real != nullptr;
     // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
     float ar[R];
@@ -1119,6 +1134,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       const bool dc = (PG::rpart(G::NPASS - 1, r) == 0) && dc_lane;
       if (dc) ar[r] = fabsf(v[r].x);  // slot 0 packs (X[0], X[N/2]), both real
     }
+    prio_lo<32>();
     MGX_MARK(amp_done);
     wave_sync();  // the last exchange's reads are done: the slot buffer is free
     if (want_cplx) {
@@ -1171,6 +1187,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) av[jj] = amp[pa(R * lane + jj)];
   prio_lo<2>();
+  prio_hi<64>();
   MGX_MARK(amp_row_done);
   // The moment and log sums only as far as a feature reads them (need_mom: 0 none, 1 S1 for
   // centroid / slope, 2 S1..S4 and sum log2 a); the amplitude total T0 always (S0, rolloff,
@@ -1217,6 +1234,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     for (int jj = 0; jj < R; ++jj) T0 += (double)av[jj];
   }
   MGX_MARK(moments_done);
+  prio_hi<8>();
   wave_sync();  // every lane has read the amplitude row: the buffer takes the prefix sums next
   FrameRec& rec = recs[fb];
   // Moments S1..S4 (bin-offset polynomial shift of the local partials) and sum log2 a:
@@ -1332,6 +1350,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     wave_sync();
     mom_reduce();
   }
+  prio_lo<8>();
   MGX_MARK(frame_end);
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
 }
@@ -1552,6 +1571,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     // Lane ids and the argument pointer are re-derived so that nothing phase 2 needs is
     // hoisted out of the batch loop (it would stay live across the FFT).
     MGX_MARK(phase2_start);
+    prio_hi<4>();
     {
       KArgs* q = args_ptr();
       const int l2 = opaque(lane);
@@ -1661,6 +1681,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         else gbl(static_cast<float*>(dst))[f] = (float)v;
       }
     }
+    prio_lo<4>();
     MGX_MARK(phase2_end);
     wave_sync();  // records and slot buffer are reused by the next batch
   }
