@@ -1,0 +1,1860 @@
+// Fused per-frame feature extraction for gfx950 (MI355X).
+//
+// One persistent launch processes a batch of frames. Each of the 4 waves of a 256-thread
+// workgroup loops over its own batches of FPW frames:
+//
+//  Phase 1 (one wave per frame, the next frame prefetched mid-frame):
+//    load + rms/energy/zcr      src/extractors/rms.js, energy.js, zcr.js
+//    window                     src/meyda.js:158-168
+//    FFT                        lib/jsfft/fft.js:123-208, restated as a Hermitian
+//                               half-spectrum radix-2 network: the
+//                               frame is real, so each stage output block is kept as
+//                               N/2 complex "slots"; every stage is rounded to
+//                               float32 exactly where jsfft stores to Float32Array,
+//                               with float64 butterflies.
+//    amplitude                  src/meyda.js:104-114 -> the wave's LDS slot buffer
+//    per-frame reductions       moments (src/utils.js:1-11), log sum
+//                               (spectralFlatness.js), prefix sums (spectralRolloff.js,
+//                               loudness band sums loudness.js:47-66), DPP wave sums
+//    mel filterbank             mfcc.js:40-62 as a segmented scan over the bins (7 %
+//                               dense: no dense contraction for the matrix cores, §4.3)
+//  Phase 2 (the wave, over its FPW-frame batch):
+//    specific loudness          loudness.js:55-63 (x^0.23, float32 store)
+//    log mel + DCT              mfcc.js:64-93: the 13 x 26 DCT, the path's one dense
+//                               contraction, on the FP64 matrix cores (v_mfma_f64_4x4x4_4b:
+//                               16 coefficients x the batch's 4 frames per instruction);
+//                               MGX_FLAG_DCT_SEQUENTIAL keeps the reference's sequential
+//                               VALU order instead
+//    scalar features            spectral*.js, perceptual*.js
+//
+// Compiled with -ffp-contract=off: every fused multiply-add below is explicit.
+#include "mgx_internal.h"
+
+namespace mgx {
+namespace {
+
+typedef const __attribute__((address_space(1))) double2* GTw;
+typedef const __attribute__((address_space(1))) float2* GTwf;
+typedef const __attribute__((address_space(1))) double* GD;
+typedef const __attribute__((address_space(1))) float* GF;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr double kS = 0.7071067811865476;  // Math.SQRT1_2 (lib/jsfft/fft.js:10)
+constexpr float kSf = 0.70710677f;
+constexpr double kLn2 = 0.6931471805599453;
+
+// Tuning knobs (-DMGX_...) select among equivalent forms measured in DESIGN.md; every
+// setting computes the same results. Timing ablations that drop work are not in this file:
+// tools/ablate.py builds them from a patched copy.
+
+constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v >> 1); }
+constexpr int rev_bits(int x, int bits) {
+  int r = 0;
+  for (int i = 0; i < bits; ++i) r = (r << 1) | ((x >> i) & 1);
+  return r;
+}
+
+// Padded slot address of an FFT exchange: loc + sum k (loc >> s), additive over the
+// disjoint lane and register bits of a location, so phys(lane part) + phys(register part)
+// (the register part an immediate offset). Chosen per N by a search over the LDS bank
+// rule of ds_write2_b64 / ds_read2_b64 (4 groups of 16 lanes, banks (a/4) mod 32): the
+// exchanges then take the conflict-free minimum of LDS cycles at N = 512, 1024 and 2048.
+template <int N>
+__host__ __device__ constexpr int phys(int loc) {
+  return N == 256 ? loc + 2 * (loc >> 4) + (loc >> 6)
+       : N == 512 ? loc + 4 * (loc >> 4) + (loc >> 6)
+       : N == 1024 ? loc + 2 * (loc >> 4) + (loc >> 7)
+       : loc + (loc >> 6);
+}
+
+template <int N>
+struct Geo {
+  static constexpr int L = N / 2;           // slots per frame == amplitude bins
+  static constexpr int R = L / 64;          // slots per lane
+  static constexpr int SB = ilog2c(L);      // slot-location bits
+  static constexpr int RB = ilog2c(R);      // register bits
+  static constexpr int NPASS = (SB + RB - 1) / RB;
+  static constexpr int CH = N / 64;         // 64-sample input chunks per frame
+#ifndef MGX_FPW
+  static constexpr int FPW = 4;             // frames per wave batch (phase 2 works on a wave batch)
+#else
+  static constexpr int FPW = MGX_FPW;
+#endif
+  static constexpr int FB = 4 * FPW;        // frames per workgroup iteration
+  // Register budget (VGPRs + AGPRs): 4 waves/SIMD (<= 128) up to N = 1024, where LDS
+  // allows 4 workgroups per CU; 3 waves (<= 168) at N = 2048 (without the frame prefetch:
+  // measured 3 % faster than 2 waves with it). Without the bound the allocator drifts past
+  // the threshold (129 VGPRs, or 251 + 32 AGPRs) and occupancy drops.
+  // N = 256 fits 6 waves (<= 80 VGPRs; measured 2.5 % faster than 5); at N = 512 a bound
+  // of 5 waves measured slower than 4.
+#ifndef MGX_WPE1024
+#define MGX_WPE1024 4
+#endif
+#ifndef MGX_WPE512
+#define MGX_WPE512 4
+#endif
+#ifdef MGX_WPE2048
+  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? MGX_WPE512 : N <= 1024 ? MGX_WPE1024 : MGX_WPE2048;
+#else
+  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? MGX_WPE512 : N <= 1024 ? MGX_WPE1024 : 3;
+#endif
+  // Slot buffer entries (8 bytes): the padded exchange image, the natural-order half
+  // spectrum X[0..L] (complex output), the padded prefix row (pd) and the mel scratch.
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int SLOT_PHYS =
+      cmax(cmax(phys<N>(L - 1) + 1, L + 1), cmax(L + 2 * (L >> 5) + 1, 2 * (kMaxMel + 2 + 64) * 4 / 8));
+  // Moment sums through an LDS transpose (5 rows of 64 doubles per wave, row stride 72 so
+  // the rows read together fall in different banks) rather than 5 DPP wave sums: measured
+  // faster up to N = 1024 (4+ waves per SIMD), slower at 2048 (2 waves).
+#ifndef MGX_MOM_LDS_MAXN
+#define MGX_MOM_LDS_MAXN 1024
+#endif
+  static constexpr bool MOM_LDS = N <= MGX_MOM_LDS_MAXN;
+  static constexpr int MOM_STRIDE = 72;
+  // MOM_SLOT: the moment transpose runs in the wave's slot buffer right after the partials are
+  // written (one more LDS round trip, no table of its own: 11.5 KB less LDS per workgroup)
+#ifndef MGX_MOM_SLOT
+#define MGX_MOM_SLOT 1
+#endif
+  static constexpr bool MOM_SLOT = MOM_LDS && MGX_MOM_SLOT && SLOT_PHYS >= 5 * MOM_STRIDE;
+  // TW_LDS (N = 1024): the per-lane twiddles of passes >= 1 (the mixed-table entries and the
+  // generic twiddles the tame passes read) are staged in LDS once per workgroup, in the space
+  // the moment table left: LDS reads (lgkmcnt) instead of vector loads (vmcnt) in the passes
+#ifndef MGX_TW_LDS
+#define MGX_TW_LDS 1
+#endif
+  static constexpr bool TW_LDS = MGX_TW_LDS && N == 1024 && MOM_SLOT;
+  // Register prefetch of the next frame. A vector-memory wait is in issue order (vmcnt),
+  // so a table load a frame waits on (window, twiddles) also waits for a prefetch issued
+  // before it: prefetching at the start of the frame made every frame wait for the next
+  // one's HBM read at its window step (at N = 1024 loading each frame only when its wave
+  // starts it was 2.7 % faster).
+// PF = 1 loads the next frame at the start of this one; PF = 2 issues it in the middle of
+  // this frame, after the last table loads this frame waits on (twiddles: the passes are
+  // done; the mel records: issued just before), so no wait of this frame is held up by
+  // it; PF = 0 loads each frame when its wave starts it.
+#ifdef MGX_PF_ALL
+  static constexpr int PF = MGX_PF_ALL;
+#else
+#ifndef MGX_PF1024
+#define MGX_PF1024 2
+#endif
+  static constexpr int PF = N <= 256 ? 1 : N < 1024 ? 2 : N == 1024 ? MGX_PF1024 : 0;  // measured best per N
+#endif
+  // WIN_REG: the window held in registers for the whole launch (CH VGPRs) instead of loaded
+  // per frame (N = 1024, where the LDS twiddles freed the registers: 1.1-1.5 % faster, 119
+  // VGPRs; the frame prefetch at the frame's start instead, MGX_PF1024=1, 0.9-1.1 %, and both
+  // together 1.1 %)
+#ifndef MGX_WIN_REG
+#define MGX_WIN_REG 1
+#endif
+  static constexpr bool WIN_REG = MGX_WIN_REG && N == 1024;
+  static constexpr bool PREFETCH = PF != 0;
+#ifdef MGX_LPREMAT
+  static constexpr bool LPREMAT = MGX_LPREMAT;
+#else
+  static constexpr bool LPREMAT = N == 2048;  // measured: N = 2048 1 % faster, N = 256 7 % slower
+#endif
+#ifdef MGX_MIXFORM
+  static constexpr int MIX = MGX_MIXFORM;
+#else
+  static constexpr int MIX = 1;  // bfly_mixed_tame (form 0 was faster at N = 1024 at 128 live VGPRs)
+#endif
+  static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
+};
+
+// Location bits of pass p: register bits [0, m) drive location bits [q0, q0+m); the
+// six lane bits take the lowest remaining location bits; leftover register bits
+// take the rest. Pass 0 is fixed by the load: location = rev6(lane)*R + r.
+template <int N>
+struct PassGeo {
+  using G = Geo<N>;
+  static constexpr int q0(int p) { return p * G::RB; }
+  static constexpr int m(int p) { return (G::SB - q0(p)) < G::RB ? (G::SB - q0(p)) : G::RB; }
+  static constexpr int free_bit(int p, int idx) {
+    int cnt = 0;
+    for (int b = 0; b < G::SB; ++b) {
+      if (b >= q0(p) && b < q0(p) + m(p)) continue;
+      if (cnt == idx) return b;
+      ++cnt;
+    }
+    return -1;
+  }
+  static constexpr int rpart(int p, int r) {
+    int loc = 0;
+    for (int i = 0; i < G::RB; ++i) {
+      const int pos = i < m(p) ? q0(p) + i : free_bit(p, 6 + (i - m(p)));
+      loc |= ((r >> i) & 1) << pos;
+    }
+    return loc;
+  }
+  static __device__ int lanepart(int p, int lane) {
+    if (p == 0) return rev_bits(lane, 6) << G::RB;
+    int loc = 0;
+    for (int i = 0; i < 6; ++i) loc |= ((lane >> i) & 1) << free_bit(p, i);
+    return loc;
+  }
+};
+
+
+// LDS image of the tame passes' per-lane twiddles (Geo<N>::TW_LDS), in double2 entries. In
+// pass P >= 1 at N = 1024 the location bits below the pass are lane bits [0, q0) and the
+// stage bits below stage q are register bits [q0, q): the mixed pairs of stage q read entries
+// mask + la, la < 2^q0 (two double2 each: (b, c0), (t4, kL)), the generic ones mask + (la | rp),
+// rp != 0, i.e. [mask + 2^q0, mask + 2^q). Per (P, I): the mixed block, then the generic one.
+template <int N>
+struct TwLds {
+  using PG = PassGeo<N>;
+  static constexpr int mixed_n(int P) { return 2 << PG::q0(P); }
+  static constexpr int gen_n(int P, int I) { return (1 << (PG::q0(P) + I)) - (1 << PG::q0(P)); }
+  static constexpr int off(int P, int I, bool gen) {
+    int o = 0;
+    for (int p = 1; p < Geo<N>::NPASS; ++p)
+      for (int i = 0; i < PG::m(p); ++i) {
+        if (p == P && i == I) return gen ? o + mixed_n(p) : o;
+        o += mixed_n(p) + gen_n(p, i);
+      }
+    return o;
+  }
+  // after the per-stage blocks: the lane-uniform (f_x, S f_y) of each tame stage's block-start
+  // pair (the mixed table's entry N/2 - 1 + q), one double2 per stage q = q0(P) + I
+  static constexpr int fw_off(int P, int I) {
+    int o = off(Geo<N>::NPASS, 0, false);
+    for (int p = 1; p < Geo<N>::NPASS; ++p)
+      for (int i = 0; i < PG::m(p); ++i) {
+        if (p == P && i == I) return o;
+        ++o;
+      }
+    return o;
+  }
+  static constexpr int total() { return fw_off(Geo<N>::NPASS, 0); }
+};
+
+// Bank-padded layouts of the amplitude row (floats) and of its prefix sums (doubles) in
+// the slot buffer: lane l reads the row (ds_read2_b64) and writes the prefix
+// (ds_write2_b64) as R consecutive entries; both instructions serve 16 consecutive lanes
+// per LDS cycle with banks (a/4) mod 32 (MI355X_MICROARCH.md §LDS). The prefix row's 1
+// double of padding per 16 gives those 16 lanes 16 distinct bank pairs at every R (the
+// former 2 per 32 left 2-way conflicts: 32 extra LDS cycles per frame at N = 1024,
+// SQ_LDS_BANK_CONFLICT). The amplitude row keeps 4 floats per 64 (2-way on its reads): 2
+// per 32 removes those too but changed the surrounding code generation and measured
+// 2.5 % slower; the LDS is not what bounds the kernel.
+__device__ __forceinline__ int pa(int k) { return k + 4 * (k >> 6); }
+__device__ __forceinline__ int pa_inv(int k) { return k - 4 * (k / 68); }  // pa(b) = 68 (b >> 6) + (b & 63)
+__device__ __forceinline__ int pd(int d) { return d + (d >> 4); }
+
+
+// Wave priority (s_setprio) in the frame's low-ILP sections: a wave in an LDS round trip or a
+// serial chain (DPP reductions, the amplitude's conversions, phase 2's scalar steps) issues
+// ahead of the other waves, whose FFT passes have independent butterflies to fill the gaps,
+// so its latency overlaps their arithmetic instead of adding to it. MGX_PRIOSET selects the
+// regions: 1 the FFT exchanges, 2 the amplitude row's LDS round trip, 4 phase 2, 8 the
+// per-frame reductions (moment transpose, prefix and rolloff, band sums, mel scan), 16 the
+// frame start (energy/zcr, window, stage 0), 32 the amplitude, 64 the moment partials.
+// Measured (interleaved A/B, all features): 1 alone 0.5-1 % faster than none;
+// 111 (all but the frame start) another 5.0 % at N = 1024, 4.3 % at 2048, 7.4 % at 512;
+// adding 16 cost N = 512 its fifth wave per SIMD (+7 %).
+#ifndef MGX_PRIOSET
+#define MGX_PRIOSET 111
+#endif
+#ifndef MGX_PRIO_P2
+#define MGX_PRIO_P2 2
+#endif
+#ifndef MGX_PRIO_XCHG
+#define MGX_PRIO_XCHG 2
+#endif
+template <int REGION>
+__device__ __forceinline__ void prio_hi() {
+  if constexpr ((MGX_PRIOSET & REGION) != 0) __builtin_amdgcn_s_setprio(REGION == 4 ? MGX_PRIO_P2 : REGION == 1 ? MGX_PRIO_XCHG : 2);
+}
+template <int REGION>
+__device__ __forceinline__ void prio_lo() {
+  if constexpr ((MGX_PRIOSET & REGION) != 0) __builtin_amdgcn_s_setprio(0);
+}
+
+// pa(spectrum bin) of each register after the last pass, live across the whole frame loop:
+// two 16-bit entries per VGPR (MGX_KLPACK=0: one int per register; packed measured 1 %
+// faster at N = 512, 0.2 % at 1024).
+#ifndef MGX_KLPACK
+#define MGX_KLPACK 1
+#endif
+template <int N>
+struct KlTab {
+  static constexpr int R = N / 128;
+#if MGX_KLPACK
+  uint32_t w[R / 2];
+  __device__ __forceinline__ void set(int r, int v) {
+    if (r & 1) w[r >> 1] |= (uint32_t)v << 16;
+    else w[r >> 1] = (uint32_t)v;
+  }
+  __device__ __forceinline__ int operator()(int r) const { return (int)((w[r >> 1] >> (16 * (r & 1))) & 0xFFFFu); }
+#else
+  int w[R];
+  __device__ __forceinline__ void set(int r, int v) { w[r] = v; }
+  __device__ __forceinline__ int operator()(int r) const { return w[r]; }
+#endif
+};
+
+// A frame sample: read once and never again. MGX_NT_FRAMES=1: non-temporal loads (`nt`).
+// Measured: the HBM-bound time-only features 12 % faster on a 1 GiB batch (5.9 TB/s), but
+// C2's 128 MiB batch 12 % slower (with plain loads it stays resident in the 256 MiB MALL
+// across launches); no change where the kernel is VALU-bound. Plain loads by default.
+#ifndef MGX_NT_FRAMES
+#define MGX_NT_FRAMES 0
+#endif
+__device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))) float* p) {
+#if MGX_NT_FRAMES
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
+// Static instruction accounting (tools/isa_phases.py): -DMGX_MARKS puts an assembly comment
+// at each phase boundary; the default build has none.
+#ifdef MGX_MARKS
+#define MGX_MARK(tag) asm volatile(";mgxmark " #tag)
+#else
+#define MGX_MARK(tag) ((void)0)
+#endif
+
+// Wave-level LDS ordering (no global-memory fence: in-flight prefetch loads stay in flight).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// Workgroup barrier ordering LDS only. __syncthreads() also fences global memory, which
+// makes every wave drain its outstanding loads (the next frame's prefetch) at each barrier.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ double2 ld_tw_u(GTw p, int i);
+__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
+  const GD q = (GD)p;
+  return make_double2(q[2 * i], q[2 * i + 1]);
+}
+// A twiddle whose index is the same on every lane (pass 0, and every block-start pair):
+// read through the constant address space, so it is an s_load into SGPRs (scalar cache)
+// instead of a vector load through the texture path, and costs no VGPRs.
+typedef const __attribute__((address_space(4))) double* CD;
+typedef const __attribute__((address_space(4))) float* CF;
+__device__ __forceinline__ double2 ld_tw_u(GTw p, int i) {
+  const CD q = (CD)(uintptr_t)p;
+  return make_double2(q[2 * i], q[2 * i + 1]);
+}
+__device__ __forceinline__ float2 ld_twf_u(GTwf p, int i) {
+  const CF q = (CF)(uintptr_t)p;
+  return make_float2(q[2 * i], q[2 * i + 1]);
+}
+__device__ __forceinline__ float2 ld_twf(GTwf p, int i) {
+  const GF q = (GF)p;
+  return make_float2(q[2 * i], q[2 * i + 1]);
+}
+
+// ---------------------------------------------------------------- butterflies
+// Twiddle table of stage q (input blocks of 2^(q+1) samples) at offset 2^q - 1:
+// entry a holds c = SQRT1_2 * f_k(a) for the slot pair (a, a + 2^q) (entry 0: S f_0 =
+// (S, 0)); after the N/2 - 1 stage entries, entry N/2 - 1 + q holds S f_{w/2}
+// for the block-start pair, whose slots pack (X[0], X[w/2]).
+//
+// Generic pair:      lo <- s L + c R,   hi <- conj(s L - c R)
+// Block-start pair:  exactly jsfft's operations for j = 0 and j = w/2.
+template <bool FAITH, bool UNI = false>
+__device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, GTw tw, GTwf twf, int idx) {
+  if constexpr (FAITH) {
+    const double2 c = UNI ? ld_tw_u(tw, idx) : ld_tw(tw, idx);
+    const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+    const double Ar = __builtin_fma(c.x, Rr, -(c.y * Ri));
+    const double Ai = __builtin_fma(c.x, Ri, c.y * Rr);
+    lo.x = (float)__builtin_fma(kS, Lr, Ar);
+    lo.y = (float)__builtin_fma(kS, Li, Ai);
+    hi.x = (float)__builtin_fma(kS, Lr, -Ar);
+    hi.y = (float)__builtin_fma(-kS, Li, Ai);
+  } else {
+    const float2 c = UNI ? ld_twf_u(twf, idx) : ld_twf(twf, idx);
+    const float Ar = __builtin_fmaf(c.x, hi.x, -(c.y * hi.y));
+    const float Ai = __builtin_fmaf(c.x, hi.y, c.y * hi.x);
+    const float Lr = lo.x, Li = lo.y;
+    lo.x = __builtin_fmaf(kSf, Lr, Ar);
+    lo.y = __builtin_fmaf(kSf, Li, Ai);
+    hi.x = __builtin_fmaf(kSf, Lr, -Ar);
+    hi.y = __builtin_fmaf(-kSf, Li, Ai);
+  }
+}
+
+// The faithful generic pair with its twiddle already in registers (TwLds).
+__device__ __forceinline__ void bfly_generic_c(float2& lo, float2& hi, double2 c) {
+  const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+  const double Ar = __builtin_fma(c.x, Rr, -(c.y * Ri));
+  const double Ai = __builtin_fma(c.x, Ri, c.y * Rr);
+  lo.x = (float)__builtin_fma(kS, Lr, Ar);
+  lo.y = (float)__builtin_fma(kS, Li, Ai);
+  hi.x = (float)__builtin_fma(kS, Lr, -Ar);
+  hi.y = (float)__builtin_fma(-kS, Li, Ai);
+}
+
+template <bool FAITH>
+__device__ __forceinline__ void bfly_special(float2& lo, float2& hi, GTw tw, GTwf twf, int idx) {
+  // f = SQRT1_2 f_{w/2}: S (Lh + f_x Rh) as S Lh + (S f_x) Rh and S (f_y Rh) as (S f_y) Rh
+  // (one f64 rounding moved in each; the exact j = 0 sums S (L0 +- R0) stay as written)
+  if constexpr (FAITH) {
+    const double2 f = ld_tw_u(tw, idx);
+    const double L0 = lo.x, Lh = lo.y, R0 = hi.x, Rh = hi.y;
+    lo.x = (float)(kS * (L0 + R0));
+    lo.y = (float)(kS * (L0 - R0));
+    hi.x = (float)__builtin_fma(kS, Lh, f.x * Rh);
+    hi.y = (float)(f.y * Rh);
+  } else {
+    const float2 f = ld_twf_u(twf, idx);
+    const float L0 = lo.x, Lh = lo.y, R0 = hi.x, Rh = hi.y;
+    lo.x = kSf * (L0 + R0);
+    lo.y = kSf * (L0 - R0);
+    hi.x = __builtin_fmaf(kSf, Lh, f.x * Rh);
+    hi.y = f.y * Rh;
+  }
+}
+
+// A pair that is block-start on some lanes (sp) and generic on the others: both forms
+// are evaluated and selected, so the wave never diverges. The block-start form keeps
+// jsfft's exact operations (S (L + R), not S L + S R): exact cancellations to 0 (DC /
+// Nyquist of symmetric blocks) must stay 0 for spectralFlatness.
+template <bool FAITH>
+__device__ __forceinline__ void bfly_mixed(float2& lo, float2& hi, GTw tw, GTwf twf, int idx, int fidx, bool sp) {
+  if constexpr (FAITH) {
+    const double2 c = ld_tw(tw, idx);
+    const double2 f = ld_tw_u(tw, fidx);
+    const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+    const double Ar = __builtin_fma(c.x, Rr, -(c.y * Ri));
+    const double Ai = __builtin_fma(c.x, Ri, c.y * Rr);
+    const double g0 = __builtin_fma(kS, Lr, Ar), g1 = __builtin_fma(kS, Li, Ai);
+    const double g2 = __builtin_fma(kS, Lr, -Ar), g3 = __builtin_fma(-kS, Li, Ai);
+    const double s0 = kS * (Lr + Rr), s1 = kS * (Lr - Rr);
+    const double s2 = __builtin_fma(kS, Li, f.x * Ri), s3 = f.y * Ri;  // f = S f_{w/2}
+    lo.x = (float)(sp ? s0 : g0);
+    lo.y = (float)(sp ? s1 : g1);
+    hi.x = (float)(sp ? s2 : g2);
+    hi.y = (float)(sp ? s3 : g3);
+  } else {
+    const float2 c = ld_twf(twf, idx);
+    const float2 f = ld_twf_u(twf, fidx);
+    const float Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+    const float Ar = __builtin_fmaf(c.x, Rr, -(c.y * Ri));
+    const float Ai = __builtin_fmaf(c.x, Ri, c.y * Rr);
+    const float g0 = __builtin_fmaf(kSf, Lr, Ar), g1 = __builtin_fmaf(kSf, Li, Ai);
+    const float g2 = __builtin_fmaf(kSf, Lr, -Ar), g3 = __builtin_fmaf(-kSf, Li, Ai);
+    const float s0 = kSf * (Lr + Rr), s1 = kSf * (Lr - Rr);
+    const float s2 = __builtin_fmaf(kSf, Li, f.x * Ri), s3 = f.y * Ri;
+    lo.x = sp ? s0 : g0;
+    lo.y = sp ? s1 : g1;
+    hi.x = sp ? s2 : g2;
+    hi.y = sp ? s3 : g3;
+  }
+}
+
+// The mixed pair of a frame whose samples are all finite and below 2^50 in magnitude
+// (no infinity can arise in the FFT). One form serves both lane kinds, with per-lane
+// coefficients (b, c0, t4, kL) from the plan's mixed table (entry a = la | rp of the stage,
+// two double2 per entry):
+//   generic lanes (b = f_x, c0 = S f_y, t4 = S f_x, kL = -S):
+//     lo = (S fma(f_x, Rr, Lr) - c0 Ri, S fma(f_x, Ri, Li) + c0 Rr),
+//     hi = (S fma(-f_x, Rr, Lr) + c0 Ri, t4 Ri + (kL Li + c0 Rr));
+//   block-start lanes (b = 1, c0 = 0, t4 = S f_y(w/2), kL = 0): t1 = L0 + R0 and
+//     t3 = L0 - R0 exactly as jsfft, lo = (S t1, S t3), hi = (S (Lh + f_x Rh), S f_y Rh)
+//     with f = f_{w/2} (fwx: lane-uniform f_x): the two middle outputs swap places.
+// 10 f64 operations and 4 selects (2 of them per stage, shared by the stage's pairs);
+// the c0 and kL products are 0 x finite on block-start lanes, which is why L, R must be finite.
+__device__ __forceinline__ void bfly_mixed_tame(float2& lo, float2& hi, double2 m, double2 k, double fwx, bool sp) {
+  const double b2 = sp ? fwx : m.x;
+  const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+  const double ui = m.y * Ri, ur = m.y * Rr;
+  const float o1 = (float)__builtin_fma(kS, __builtin_fma(m.x, Rr, Lr), -ui);
+  const float o3 = (float)__builtin_fma(kS, __builtin_fma(-m.x, Rr, Lr), ui);
+  const float o2 = (float)__builtin_fma(kS, __builtin_fma(b2, Ri, Li), ur);
+  const float o4 = (float)__builtin_fma(k.x, Ri, __builtin_fma(k.y, Li, ur));
+  lo.x = o1;
+  lo.y = sp ? o3 : o2;
+  hi.x = sp ? o2 : o3;
+  hi.y = o4;
+}
+// The same pair with the last output selected per lane (S f_y(w/2) Ri on block-start
+// lanes): 11 f64 operations and 6 selects, no (t4, kL) — cheaper for a stage's only pair.
+[[maybe_unused]] __device__ __forceinline__ void bfly_mixed_tame1(float2& lo, float2& hi, double2 m, double2 fw, bool sp) {
+  const double b2 = sp ? fw.x : m.x;
+  const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+  const double ui = m.y * Ri, ur = m.y * Rr;
+  const float o1 = (float)__builtin_fma(kS, __builtin_fma(m.x, Rr, Lr), -ui);
+  const float o3 = (float)__builtin_fma(kS, __builtin_fma(-m.x, Rr, Lr), ui);
+  const float o2 = (float)__builtin_fma(kS, __builtin_fma(b2, Ri, Li), ur);
+  const double o4 = sp ? fw.y * Ri : __builtin_fma(-kS, __builtin_fma(-b2, Ri, Li), ur);
+  lo.x = o1;
+  lo.y = sp ? o3 : o2;
+  hi.x = sp ? o2 : o3;
+  hi.y = (float)o4;
+}
+
+// How the tame mixed pairs of a stage get (t4, kL) (Geo<N>::MIX): 0 = per pair
+// (bfly_mixed_tame1), 1 = from the plan table, 2 = computed once per stage (t4 = S b,
+// kL = -S; block start: S f_y(w/2), 0). Measured (all features): the table form is 1 % faster
+// at N = 512, 3 % at N = 2048 and 1.9 % at N = 1024 (there only once the moment and
+// amplitude changes had freed registers; before, 1.8 % slower).
+
+// One radix-2 stage on location bit q = q0(P) + I, entirely in registers.
+template <int N, int P, int I, bool FAITH, bool TAME>
+__device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm,
+                                          const double2* twl) {
+  constexpr bool LT = FAITH && TAME && Geo<N>::TW_LDS && P > 0;  // twiddles from the LDS image
+  using G = Geo<N>;
+  using PG = PassGeo<N>;
+  constexpr int q = PG::q0(P) + I;
+  constexpr int mask = (1 << q) - 1;
+  constexpr int fidx = G::L - 1 + q;  // f_{w/2} of this stage
+  const int la = lp & mask;  // 0 in pass 0
+#pragma unroll
+  for (int r = 0; r < G::R; ++r) {
+    if (r & (1 << I)) continue;
+    const int rp = PG::rpart(P, r) & mask;
+    const int hi = r | (1 << I);
+    if constexpr (P == 0) {
+      if (rp == 0) bfly_special<FAITH>(v[r], v[hi], tw, twf, fidx);
+      else bfly_generic<FAITH, true>(v[r], v[hi], tw, twf, mask + rp);
+    } else if (rp == 0) {
+      if constexpr (FAITH && TAME) {
+        // every mixed pair of the stage has rp == 0: one coefficient entry per lane and stage
+        constexpr int npairs = G::R >> (I + 1);
+        const bool sp = la == 0;
+        const double2 fw = LT ? twl[TwLds<N>::fw_off(P, I)] : ld_tw_u(twm, 2 * fidx);
+        const double2 m = LT ? twl[TwLds<N>::off(P, I, false) + 2 * la] : ld_tw(twm, 2 * (mask + la));
+        if constexpr (G::MIX == 0 || (G::MIX == 2 && npairs == 1)) {
+          bfly_mixed_tame1(v[r], v[hi], m, fw, sp);
+        } else if constexpr (G::MIX == 1) {
+          bfly_mixed_tame(v[r], v[hi], m, LT ? twl[TwLds<N>::off(P, I, false) + 2 * la + 1] : ld_tw(twm, 2 * (mask + la) + 1),
+                          fw.x, sp);
+        } else {
+          const double2 k = make_double2(sp ? fw.y : kS * m.x, sp ? 0.0 : -kS);
+          bfly_mixed_tame(v[r], v[hi], m, k, fw.x, sp);
+        }
+      }
+      else bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, fidx, la == 0);
+    } else if constexpr (LT) {
+      bfly_generic_c(v[r], v[hi], twl[TwLds<N>::off(P, I, true) + ((la | rp) - (1 << PassGeo<N>::q0(P)))]);
+    } else {
+      bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + (la | rp));
+    }
+  }
+}
+
+template <int N, int P, int I, bool FAITH, bool TAME>
+__device__ __forceinline__ void run_stages(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm,
+                                           const double2* twl) {
+  if constexpr (I < PassGeo<N>::m(P)) {
+    run_stage<N, P, I, FAITH, TAME>(v, lp, tw, twf, twm, twl);
+    run_stages<N, P, I + 1, FAITH, TAME>(v, lp, tw, twf, twm, twl);
+  }
+}
+
+// Move the slots from pass P-1's lane/register layout to pass P's through LDS.
+template <int N, int P>
+__device__ __forceinline__ void exchange(float2 (&v)[Geo<N>::R], int lp_prev, int lp_cur, float2* buf) {
+  using G = Geo<N>;
+  using PG = PassGeo<N>;
+  const int bprev = phys<N>(lp_prev), bcur = phys<N>(lp_cur);
+  MGX_MARK(xchg_begin);
+  prio_hi<1>();
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < G::R; ++r) buf[bprev + phys<N>(PG::rpart(P - 1, r))] = v[r];
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < G::R; ++r) v[r] = buf[bcur + phys<N>(PG::rpart(P, r))];
+  prio_lo<1>();
+  MGX_MARK(xchg_end);
+}
+
+template <int N, int P, bool FAITH, bool TAME>
+__device__ __forceinline__ void run_passes(float2 (&v)[Geo<N>::R], const int (&lp)[Geo<N>::NPASS],
+                                           float2* buf, GTw tw, GTwf twf, GTw twm, const double2* twl) {
+  if constexpr (P < Geo<N>::NPASS) {
+    if constexpr (P > 0) exchange<N, P>(v, lp[P - 1], lp[P], buf);
+    run_stages<N, P, 0, FAITH, TAME>(v, lp[P], tw, twf, twm, twl);
+    run_passes<N, P + 1, FAITH, TAME>(v, lp, buf, tw, twf, twm, twl);
+  }
+}
+
+// ------------------------------------------------------- DPP wave reductions
+// Cross-lane moves on the VALU (no LDS round trips): quad_perm / row mirrors /
+// row shifts / row broadcasts of gfx9 DPP, applied to both halves of a double.
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROW_MASK, BANK_MASK, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROW_MASK, BANK_MASK, true);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// Sum over the 64 lanes; the result is wave-uniform.
+__device__ __forceinline__ double wave_sum(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror: every lane holds its row's sum
+  v += dpp_d<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3 hold rows 0+1, 2+3
+  v += dpp_d<0x143, 0xC>(v);  // row_bcast:31 -> row 3 holds the total
+  return readlane_d(v, 63);
+}
+
+// Inclusive prefix sum over the lanes.
+__device__ __forceinline__ double wave_inclusive_scan(double v) {
+  v += dpp_d<0x111>(v);            // row_shr:1
+  v += dpp_d<0x112>(v);            // row_shr:2
+  v += dpp_d<0x114>(v);            // row_shr:4
+  v += dpp_d<0x118>(v);            // row_shr:8
+  v += dpp_d<0x142, 0xA>(v);       // row_bcast:15 -> rows 1, 3
+  v += dpp_d<0x143, 0xC>(v);       // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// Amplitude of one slot: src/meyda.js:104-114, sqrt(re^2 + im^2) in double, stored to float32.
+template <bool FAITH>
+__device__ __forceinline__ float slot_amp(float re, float im) {
+  if constexpr (FAITH) {
+    // s = re^2 + im^2 lies in [2^-298, 2^256) or is 0/inf/NaN, so the library sqrt's
+    // range scaling is not needed: rsq seed + the two-residual refinement (full double
+    // accuracy), then 0/inf/NaN pass through.
+    const double xr = re, xi = im;
+    const double s = __builtin_fma(xr, xr, xi * xi);
+    const double y = __builtin_amdgcn_rsq(s);
+    double g = s * y, h = 0.5 * y;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, s);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, s);
+    g = __builtin_fma(d, h, g);
+    return (float)((s > 0.0 && s < __builtin_huge_val()) ? g : s);
+  } else {
+    return sqrtf(__builtin_fmaf(re, re, im * im));
+  }
+}
+
+// The same amplitude through the f32 hardware reciprocal square root plus one f64 Heron
+// correction (about half the issue cycles: v_rsq_f64 alone costs 16 cycles per wave, the
+// f64 Newton chain 9 more f64 operations). s = re^2 + im^2 exactly as above; q = rsq(s) in
+// f32, y = s q (~2^-22 relative), r = s - y^2 exactly in f64, then g = y + r q / 2 as one
+// float32 FMA of (float)r (~2^-43 relative before its single rounding): equal to the
+// correctly rounded sqrt unless sqrt(s) lies within 2^-43 of a float32 rounding boundary
+// (~2^-19 of the bins; those move by one ulp). ok is false when s leaves [2^-80, 2^120]
+// (0, tiny -- where r would be a float32 denormal --, huge, inf, NaN): the caller then
+// redoes the wave's frame with slot_amp.
+__device__ __forceinline__ float slot_amp_rsq(float re, float im, bool& ok) {
+  const double xr = re, xi = im;
+  const double s = __builtin_fma(xr, xr, xi * xi);
+  const float sf = (float)s;
+  const float q = __builtin_amdgcn_rsqf(sf);
+  const float yf = sf * q;
+  const double y = yf;
+  const float r = (float)__builtin_fma(-y, y, s);
+  const float a = __builtin_fmaf(r, 0.5f * q, yf);
+  // s in [2^-80, 2^120] <=> a in [2^-40, 2^60] (outside, the rsq seed is a denormal, 0,
+  // inf or NaN and so is a, or a is out of range): float32 compares instead of f64 ones
+  ok = a >= 0x1p-40f && a <= 0x1p60f;
+  return a;
+}
+
+struct FrameRec {
+  double S[5];      // sum_k k^p a_k, p = 0..4 (S[0] = sum a_k)
+  double ln2sum;    // sum_k log2 a_k (must follow S[4]: written as (&S[1])[4])
+  double energy;    // sum x^2
+  double band[kBark];
+  float lm[kMaxMel];  // mel band energies, then their logs (zero-padded to a multiple of 8)
+  int zcr;
+  int roll_m;
+  double pad;       // 520 bytes: phase 2 reads across frames hit distinct LDS banks (512 would not)
+};
+
+// Math.pow(x, 0.23) rounded to float32 (loudness.js:62), without the f64 exp/log
+// routines: x = m 2^e with m in [1, 2); log2 m = log2(m_hi) + m_lo / (m_hi ln 2) from the
+// f32 hardware log (m_hi = (float)m); y = 0.23 log2 x in double; 2^y = 2^floor(y) 2^frac(y)
+// with the f32 hardware exp2 on [0, 1). Relative error ~1e-7 (a float32 ulp or two).
+__device__ __forceinline__ float pow023(double x) {
+  // 0, inf, NaN (a band sum is never negative): pow's values, without the library routine
+  // (its f64 log/exp code would run for a whole wave whenever one band of a frame is silent)
+  if (!(x > 0.0 && x < __builtin_huge_val())) return x == 0.0 ? 0.0f : x > 0.0 ? __builtin_huge_valf() : (float)x;
+  int e;
+  const double m = 2.0 * frexp(x, &e);  // [1, 2)
+  const float mh = (float)m, ml = (float)(m - (double)mh);
+  // (the correction ml / (mh ln 2) is ~2^-24 relative: a hardware reciprocal suffices)
+  const float l2m = __builtin_fmaf(ml * 1.4426950408889634f, __builtin_amdgcn_rcpf(mh), __builtin_amdgcn_logf(mh));
+  const double y = 0.23 * ((double)(e - 1) + (double)l2m);
+  const double n = floor(y);
+  return ldexpf(__builtin_amdgcn_exp2f((float)(y - n)), (int)n);
+}
+
+// Math.log(x) of a float32, rounded to float32 (mfcc.js:64): ln x = (e + log2 m) ln 2 with
+// x = m 2^e, m in [1, 2) exact and log2 m from the f32 hardware log; |error| ~4e-8 absolute.
+__device__ __forceinline__ float ln_f32(float x) {
+  // 0 -> -inf, inf -> inf, NaN -> NaN (a mel energy is never negative), as Math.log
+  if (!(x > 0.0f && x < __builtin_huge_valf())) return x == 0.0f ? -__builtin_huge_valf() : x;
+  int e;
+  const float m = 2.0f * frexpf(x, &e);
+  return (float)(((double)(e - 1) + (double)__builtin_amdgcn_logf(m)) * kLn2);
+}
+
+// Arguments live in the kernarg segment (constant address space 4: scalar loads).
+typedef const KernelArgs __attribute__((address_space(4))) KArgs;
+
+// Kernel arguments read through an opaque pointer into the kernarg segment: the compiler
+// re-loads fields (scalar loads, K$ hits) after each acquisition point instead of keeping
+// ~40 pointers resident in registers across the whole batch loop.
+__device__ __forceinline__ KArgs* args_ptr() {
+  KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+// Pointers read through args_ptr() are generic; re-type them as global (address space 1)
+// so loads and stores are global_* (vmcnt only), never flat_* (which also ties up lgkmcnt).
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gbl(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void put_scalar(KArgs* a, int i, uint64_t f, double v) {
+  if (a->out.scalars[i]) gbl(static_cast<T*>(a->out.scalars[i]))[f] = (T)v;
+}
+
+template <int N>
+struct Lds {
+  using G = Geo<N>;
+  // One slot buffer per wave: FFT exchanges, then the frame's amplitude row, its prefix
+  // sums and the mel segment sums (mel_energies) in turn.
+  static constexpr size_t slot_off = 0;
+  static constexpr size_t slot_bytes = (size_t)4 * G::SLOT_PHYS * 8;
+  static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2 + 64) * 4, "mel scratch must fit");
+  // Per wave, the 5 x 64 table of moment partials (transposed reduction, N <= 512).
+  static constexpr size_t mom_off = slot_off + slot_bytes;
+  static constexpr size_t mom_bytes = (G::MOM_LDS && !G::MOM_SLOT) ? (size_t)4 * 5 * G::MOM_STRIDE * 8 : 0;
+  static_assert(!G::MOM_SLOT || (size_t)G::SLOT_PHYS >= (size_t)5 * G::MOM_STRIDE, "moment table must fit the slot buffer");
+  // Frame records: FPW per wave.
+  static constexpr size_t rec_off = mom_off + mom_bytes;
+  // Kernel constants read per lane, staged once per workgroup: the 13 scalar output
+  // pointers and the 25 bark band limits. Read from LDS (lgkmcnt) rather than global
+  // memory: a vector-memory wait is in issue order (vmcnt), so a global read here would
+  // also wait for every output store and frame load issued before it.
+  static constexpr size_t kc_off = rec_off + (size_t)G::FB * sizeof(FrameRec);
+  static constexpr size_t kc_bytes = 16 * 8 + 32 * 4;
+  // The tame passes' per-lane twiddles (Geo<N>::TW_LDS, TwLds), staged once per workgroup.
+  static constexpr size_t twl_off = kc_off + kc_bytes;
+  static constexpr size_t twl_bytes = G::TW_LDS ? (size_t)TwLds<N>::total() * 16 : 0;
+  static_assert(twl_off % 16 == 0, "double2 alignment");
+  // The DCT table (mfcc.js:67-83), staged once per workgroup, sized per plan.
+  static constexpr size_t dct_off = twl_off + twl_bytes;
+  static size_t bytes(int ncoef, int nfilt) { return dct_off + (size_t)ncoef * ((nfilt + 7) & ~7) * 4; }
+};
+
+// DPP move of one dword (bound_ctrl: lanes without a source read 0).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, true));
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, true);
+}
+
+// Mel band energies of one frame, mfcc.js:40-62: E_j = sum_k w_jk p_k, p_k = a_k^2 (float32).
+// The triangular filters split the bins into segments m = [b_m, b_{m+1}): every bin
+// belongs to one segment, and band j = (rising half on segment j) + (falling half on
+// segment j+1). So E_j = U_j + D_{j+1} with U_m = sum_{k in m} up(k) p_k and
+// D_m = sum_{k in m} dn(k) p_k: two segmented sums over the bins, computed as in-lane
+// runs plus one segmented scan across the lanes. Where the segments start
+// does not depend on the frame, so every branch of that logic is a plan table
+// (plan.cpp mel_lane_tables): per bin a keep factor (0 restarts the sums) and the scratch
+// slot the running sums are stored to, per lane the keeps of the six scan steps and the two
+// slots of the head and tail totals. No selects, one packed multiply and one packed FMA per
+// bin, one DPP-fused FMA per scan step and sum. No cross-segment sums are formed, so there
+// is no cancellation; the sums are float32 like the reference's Float32Array accumulation,
+// in a different order.
+// The lane's record of the frame-independent mel tables (plan.cpp mel_lane_tables), issued
+// before the moment sums so that the load latency hides behind the reductions.
+template <int N>
+struct MelTab {
+  static constexpr int R = Geo<N>::R, W = mel_rec_words(R), B = (R + 3) / 4;
+  uint32_t w[W];
+  __device__ __forceinline__ void load(KArgs* ap, int lane) {
+    const auto src = gbl(ap->t.mel_rec) + W * lane;
+#pragma unroll
+    for (int i = 0; i < W; ++i) w[i] = src[i];
+  }
+  __device__ __forceinline__ float rise(int jj) const { return __builtin_bit_cast(float, w[jj]); }
+  __device__ __forceinline__ uint32_t slot(int jj) const { return (w[R + jj / 4] >> (8 * (jj % 4))) & 0xFFu; }
+  __device__ __forceinline__ float keep(int jj) const { return (float)((w[R + B + jj / 4] >> (8 * (jj % 4))) & 0xFFu); }
+  __device__ __forceinline__ float scan_keep(int s) const { return (float)((w[R + 2 * B + s / 4] >> (8 * (s % 4))) & 0xFFu); }
+  __device__ __forceinline__ uint32_t head_slot() const { return (w[R + 2 * B + 1] >> 16) & 0xFFu; }
+  __device__ __forceinline__ uint32_t tail_slot() const { return w[R + 2 * B + 1] >> 24; }
+};
+
+// Mel band energies of one frame, mfcc.js:40-62: E_j = sum_k w_jk p_k, p_k = a_k^2 (float32).
+// The triangular filters split the bins into segments m = [b_m, b_{m+1}): every bin
+// belongs to one segment, and band j = (rising half on segment j) + (falling half on
+// segment j+1). So E_j = U_j + D_{j+1} with U_m = sum_{k in m} up(k) p_k and
+// D_m = sum_{k in m} dn(k) p_k: two segmented sums over the bins, computed as in-lane
+// runs plus one segmented scan across the lanes. Where the segments start
+// does not depend on the frame, so every branch of that logic is a plan table (MelTab):
+// per bin a keep factor (0 restarts the sums) and the scratch slot the running sums are
+// stored to, per lane the keeps of the six scan steps and the slots of the head and tail
+// totals. No selects: per bin a packed multiply and a packed FMA, per scan step two DPP
+// moves and a packed FMA. No cross-segment sums are formed, so there is no cancellation;
+// the sums are float32 like the reference's Float32Array accumulation, in a different order
+// (and the falling weight is 1 - rising in float32, within an ulp of the f64 ratio).
+template <int N>
+__device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>::R], int lane, float2* buf,
+                                             FrameRec& rec, const MelTab<N>& mt) {
+  constexpr int R = Geo<N>::R;
+  const int nf = ap->nfilt;
+  float2* mud = buf;  // (U, D) of segments 0..nf+1, then the 64 head partials (kMelHead)
+  wave_sync();  // band-sum reads of the prefix buffer are done
+  float2* mine = mud + lane;  // segment slot `lane` (and lane + 64), head slot kMelHead + lane
+  if (lane < nf + 2) mine[0] = make_float2(0.0f, 0.0f);
+  if (lane + 64 < nf + 2) mine[64] = make_float2(0.0f, 0.0f);
+  wave_sync();
+  f32x2 acc = {0.0f, 0.0f};
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) {
+    const float p = av[jj] * av[jj];  // powerSpectrum.js
+    mud[mt.slot(jj)] = make_float2(acc.x, acc.y);
+    const float up = mt.rise(jj), kp = mt.keep(jj);
+    const f32x2 w = {up, 1.0f - up}, pp = {p, p}, kk = {kp, kp};
+    acc = __builtin_elementwise_fma(w, pp, acc * kk);
+  }
+  // segmented inclusive scan of the lane tails: s += keep_s * s_src (keep_s = 0 once the
+  // lanes summed so far hold a segment start; a missing source lane reads 0)
+  f32x2 sc = acc;
+  auto step = [&](float u, float d, int s) {
+    const f32x2 src = {u, d}, ks = {mt.scan_keep(s), mt.scan_keep(s)};
+    sc = __builtin_elementwise_fma(src, ks, sc);
+  };
+  step(dpp_f<0x111>(sc.x), dpp_f<0x111>(sc.y), 0);  // row_shr:1
+  step(dpp_f<0x112>(sc.x), dpp_f<0x112>(sc.y), 1);  // row_shr:2
+  step(dpp_f<0x114>(sc.x), dpp_f<0x114>(sc.y), 2);  // row_shr:4
+  step(dpp_f<0x118>(sc.x), dpp_f<0x118>(sc.y), 3);  // row_shr:8
+  step(dpp_f<0x142, 0xA>(sc.x), dpp_f<0x142, 0xA>(sc.y), 4);  // row_bcast:15 (rows 1, 3)
+  step(dpp_f<0x143, 0xC>(sc.x), dpp_f<0x143, 0xC>(sc.y), 5);  // row_bcast:31 (rows 2, 3)
+  const float xu = dpp_f<0x138>(sc.x), xd = dpp_f<0x138>(sc.y);  // exclusive: carry into this lane (wave_shr:1)
+  const float2 hp = mine[kMelHead];
+  mud[mt.head_slot()] = make_float2(xu + hp.x, xd + hp.y);  // the segment this lane's first start closes
+  mud[mt.tail_slot()] = make_float2(sc.x, sc.y);           // lane 63: the segment still open at the last bin
+  wave_sync();
+  if (lane < nf) rec.lm[lane] = mine[0].x + mine[1].y;  // nf <= kMaxMel = 64
+}
+
+// Bark-band sums and mel energies of a frame with a non-finite amplitude, summed exactly
+// as the reference does (see frame_phase1). The amplitude row is rewritten to the slot buffer.
+template <int N>
+__device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av)[Geo<N>::R], int lane,
+                                                               float2* buf, FrameRec& rec) {
+  constexpr int L = N / 2, R = Geo<N>::R;
+  float* amp = reinterpret_cast<float*>(buf);
+  wave_sync();  // prefix reads (band sums) are done
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) amp[R * lane + jj] = av[jj];
+  wave_sync();
+  if (lane < kBark) {  // loudness.js:47-66: sumArray over [lim_b, lim_{b+1}) in double
+    const auto lim = gbl(ap->t.bblim);
+    double sum = 0.0;
+    for (int k = lim[lane]; k < lim[lane + 1]; ++k) sum += (double)amp[k];
+    rec.band[lane] = sum;
+  }
+  if (ap->need_mfcc) {  // mfcc.js:53-62: every bin, double weight x float power, float32 sum
+    const int nf = ap->nfilt;
+    const auto b = gbl(ap->t.mel_bins);
+    for (int j = lane; j < nf; j += 64) {
+      const int b0 = b[j], b1 = b[j + 1], b2 = b[j + 2];
+      float e = 0.0f;
+      for (int k = 0; k < L; ++k) {
+        double w = 0.0;
+        if (k >= b0 && k < b1) w = (double)(k - b0) / (b1 - b0);
+        if (k >= b1 && k < b2) w = (double)(b2 - k) / (b2 - b1);
+        const float p = amp[k] * amp[k];
+        e = (float)((double)e + w * (double)p);
+      }
+      rec.lm[j] = e;
+    }
+  }
+}
+
+// MGX_FLAG_MFCC_REFERENCE: the mel band energies in the reference's own order (mfcc.js:40-62).
+// Lane j < nfilt owns band j and walks its bins in ascending order: the weight
+// (k - b_j) / (b_{j+1} - b_j) on the rising segment, (b_{j+2} - k) / (b_{j+2} - b_{j+1}) on the
+// falling one, each the correctly rounded double quotient; the product with the float32 power
+// rounded to double; the sum rounded to double and stored to the Float32Array accumulator.
+// Bins outside [b_j, b_{j+2}) carry weight 0 in the reference and add exactly +0 there (finite
+// frames only; non-finite ones take nonfinite_frame_sums). The quotient t/d of two small
+// integers comes from r = 1/d (IEEE, once per segment) as q0 = t r, e = t - q0 d (exact by
+// FMA), q0 + e r: the correctly rounded quotient for every 0 <= t <= d <= 4096 (checked
+// exhaustively on the CPU; tests/test_capi_host.py), with no division in the loop.
+template <int N>
+__device__ __forceinline__ void mel_reference_order(KArgs* ap, const float (&av)[Geo<N>::R], int lane, float2* buf,
+                                                    FrameRec& rec) {
+  constexpr int R = Geo<N>::R;
+  double* prow = reinterpret_cast<double*>(buf);  // the frame's power spectrum, float32 values in double
+  wave_sync();  // band-sum reads of the prefix buffer are done
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) prow[R * lane + jj] = (double)(av[jj] * av[jj]);  // powerSpectrum.js
+  wave_sync();
+  const int nf = ap->nfilt;
+  if (lane < nf) {
+    const auto b = gbl(ap->t.mel_bins);
+    constexpr int L = N / 2;  // the reference sums bins j < N/2 only
+    const int b0 = min(b[lane], L), b1 = min(b[lane + 1], L), b2 = min(b[lane + 2], L);
+    double acc = 0.0;  // the Float32Array element, held exactly in double
+    // One segment, 4 bins per step: the weights and products of a step are independent, only
+    // the accumulator is serial. Bins past the segment's end contribute an exact +0 (their
+    // product is selected away, never multiplied: the slot buffer holds other data there).
+    auto segment = [&](int k0, int k1, bool rising) {
+      if (k1 <= k0) return;
+      const double d = (double)(k1 - k0), r = 1.0 / d;
+      for (int k = k0; k < k1; k += 4) {
+        double pr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double t = (double)(rising ? k + u - k0 : k1 - k - u);
+          const double q0 = t * r;
+          const double w = __builtin_fma(__builtin_fma(-q0, d, t), r, q0);
+          const double p = prow[k + u];
+          pr[u] = k + u < k1 ? w * p : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = (double)(float)(acc + pr[u]);  // two double roundings, the float32 store
+      }
+    };
+    segment(b0, b1, true);
+    segment(b1, b2, false);
+    rec.lm[lane] = (float)acc;
+  }
+}
+
+// One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
+template <int N, bool FAITH, bool LITERAL, bool SUB>
+__device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
+                                             int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
+                                             bool dc_lane, float2* buf, double* mom, FrameRec* recs,
+                                             const int* klim, float (&xn)[Geo<N>::PREFETCH ? Geo<N>::CH : 1],
+                                             GF next, const double2* twl, const float (&wreg)[Geo<N>::CH]) {
+  using G = Geo<N>;
+  using PG = PassGeo<N>;
+  constexpr int L = G::L, R = G::R, CH = G::CH;
+  float* amp = reinterpret_cast<float*>(buf);  // the frame's amplitude row, once the FFT is done
+  double* pbuf = reinterpret_cast<double*>(buf);
+
+  // mid-frame prefetch of the next frame (G::PF == 2), after the mel records are issued
+  // (frames without spectral features: right away)
+  auto prefetch_next = [&]() {
+    if constexpr (G::PF == 2) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) xn[c] = ld_frame(next + c * 64);
+    }
+  };
+  if (!ap->need_spectrum) prefetch_next();  // time-only features: no table loads follow
+  // The window's table loads are issued before the energy / zcr reductions, so their latency
+  // hides behind them rather than at the window step after the reductions' branches (1 %
+  // faster at N = 512, equal at 1024 and 2048; a lane-major table read as 16-byte loads was
+  // 2-5 % slower at 512 and 2048).
+  float wv[CH];
+  if (G::WIN_REG) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) wv[c] = wreg[c];
+  } else if (ap->need_spectrum) {
+    const GF w = gbl(ap->t.window);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) wv[c] = w[c * 64 + lane];
+  }
+  MGX_MARK(energy_zcr);
+  prio_hi<16>();
+  // rms.js / energy.js: sum of squares; zcr.js: sign changes of adjacent samples,
+  // `x >= 0` vs `x < 0` (so -0 is non-negative and NaN never counts).
+  // Sum of squares as packed float32 FMAs over pairs of chunks; zcr from one ballot per
+  // chunk (x < 0): without NaN samples, x >= 0 is its complement. A NaN sample makes that
+  // lane's sum of squares NaN, and such frames count with both comparisons.
+  f32x2 e2 = {0.0f, 0.0f};
+#pragma unroll
+  for (int c = 0; c < CH; c += 2) {
+    const f32x2 xv = {x[c], x[c + 1]};
+    e2 = __builtin_elementwise_fma(xv, xv, e2);
+  }
+  const float e32 = e2.x + e2.y;
+  int z = 0;
+  uint64_t pge = 0, plt = 0;
+  if (__ballot(e32 != e32)) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const uint64_t g = __ballot(x[c] >= 0.0f), l = __ballot(x[c] < 0.0f);
+      z += __popcll(((g & (l >> 1)) | (l & (g >> 1))) & 0x7FFFFFFFFFFFFFFFull);
+      if (c > 0) z += (int)((((pge >> 63) & l) | ((plt >> 63) & g)) & 1ull);
+      pge = g;
+      plt = l;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const uint64_t l = __ballot(x[c] < 0.0f), g = ~l;
+      z += __popcll(((g & (l >> 1)) | (l & (g >> 1))) & 0x7FFFFFFFFFFFFFFFull);
+      if (c > 0) z += (int)((((pge >> 63) & l) | ((plt >> 63) & g)) & 1ull);
+      pge = g;
+      plt = l;
+    }
+  }
+  // float32 partial sums are within 1e-6 relative of the double sum; a wave whose
+  // partials leave [2^-100, 2^100] (silence, denormal or huge input) redoes it in double.
+  double e;
+  if (__ballot(!(e32 >= 0x1p-100f && e32 <= 0x1p100f))) {
+    double e64 = 0.0;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) e64 = __builtin_fma((double)x[c], (double)x[c], e64);
+    e = wave_sum(e64);
+  } else {
+#ifdef MGX_ENERGY_F64SUM
+    e = wave_sum((double)e32);
+#else
+    // the 64 lane partials summed in float32 too (6 DPP-fused adds instead of 6 f64 DPP
+    // steps): ~4e-7 relative at most on top of the partials' own ~1e-6, against the 1e-5 bar
+    float t = e32;
+    t += dpp_f<0xB1>(t);
+    t += dpp_f<0x4E>(t);
+    t += dpp_f<0x141>(t);
+    t += dpp_f<0x140>(t);
+    t += dpp_f<0x142, 0xA>(t);
+    t += dpp_f<0x143, 0xC>(t);
+    e = (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
+#endif
+  }
+  if (lane == 0) {
+    recs[fb].energy = e;
+    recs[fb].zcr = z;
+  }
+  if (!ap->need_spectrum) {  // (the prefetch was issued at the top: nothing to wait on)
+    prio_lo<16>();
+    return;
+  }
+  // Every sample finite and |x| <= 2^50 (each lane's sum of squares <= 2^100, not NaN):
+  // no stage of the FFT can reach an infinity (bfly_mixed_tame).
+  const bool tame = !__ballot(!(e32 <= 0x1p100f));
+  MGX_MARK(window);
+
+  // src/meyda.js:158-168: windowed[i] = sig[i] * w[i], stored to Float32Array
+  // (the exact double product rounded once == a float32 multiply).
+  {
+#pragma unroll
+    for (int c = 0; c < CH; c += 2) {  // packed float32 multiplies
+      const f32x2 xv = {x[c], x[c + 1]}, wp = {wv[c], wv[c + 1]};
+      const f32x2 y = xv * wp;
+      x[c] = y.x;
+      x[c + 1] = y.y;
+    }
+  }
+  if constexpr (LITERAL) {
+    // The snapshot never transforms per buffer: |w x| is the "spectrum".
+#pragma unroll
+    for (int c = 0; c < R; ++c) amp[pa(c * 64 + lane)] = fabsf(x[c]);
+  } else {
+    // Stage 0 (jsfft width 1) at load: slot j = rev(e) pairs x[e] with x[e + N/2].
+    float2 v[R];
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      const int r = rev_bits(c, G::RB);
+      if constexpr (FAITH) {
+        const double xa = x[c], xb = x[c + R];
+        v[r].x = (float)(kS * (xa + xb));
+        v[r].y = (float)(kS * (xa - xb));
+      } else {
+        v[r].x = kSf * (x[c] + x[c + R]);
+        v[r].y = kSf * (x[c] - x[c + R]);
+      }
+    }
+    prio_lo<16>();
+    MGX_MARK(stage0_done);
+    GTw tw = gbl(ap->t.tw);
+    GTwf twf = gbl(ap->t.twf);
+    GTw twm = gbl(ap->t.twm);
+    // G::LPREMAT: the lane parts are recomputed from the lane id in each frame (a few bit
+    // operations) instead of being kept live across the frame loop, where the allocator
+    // spilled them and reloaded from scratch in the middle of the FFT (a vector-memory wait).
+    int lpf[G::NPASS];
+#pragma unroll
+    for (int p = 0; p < G::NPASS; ++p) lpf[p] = G::LPREMAT ? PG::lanepart(p, opaque(lane)) : lp[p];
+    if constexpr (FAITH) {
+      // pass 0 has no mixed pairs; the later passes take the tame form when they can
+      run_stages<N, 0, 0, FAITH, false>(v, lpf[0], tw, twf, twm, twl);
+      MGX_MARK(pass0_done);
+      if (tame) run_passes<N, 1, FAITH, true>(v, lpf, buf, tw, twf, twm, twl);
+      else run_passes<N, 1, FAITH, false>(v, lpf, buf, tw, twf, twm, twl);
+    } else {
+      run_passes<N, 0, FAITH, false>(v, lpf, buf, tw, twf, twm, twl);
+    }
+    MGX_MARK(fft_done);
+    prio_hi<32>();
+    const bool want_cplx = ap->out.complex_real != nullptr;
+    // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
+    float ar[R];
+    if constexpr (FAITH) {
+      bool ok = true;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        bool okr;
+        ar[r] = slot_amp_rsq(v[r].x, v[r].y, okr);
+        // (the packed DC/Nyquist slot is replaced below: its range does not matter)
+        if (PG::rpart(G::NPASS - 1, r) == 0) okr = okr || dc_lane;
+        ok = ok && okr;
+      }
+      if (__ballot(!ok)) {  // a zero, tiny, huge or non-finite |X|^2 somewhere in the frame
+#pragma unroll
+        for (int r = 0; r < R; ++r) ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool dc = (PG::rpart(G::NPASS - 1, r) == 0) && dc_lane;
+      if (dc) ar[r] = fabsf(v[r].x);  // slot 0 packs (X[0], X[N/2]), both real
+    }
+    prio_lo<32>();
+    MGX_MARK(amp_done);
+    wave_sync();  // the last exchange's reads are done: the slot buffer is free
+    if (want_cplx) {
+      // natural-order half spectrum X[0..N/2] in the slot buffer
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const bool dc = (PG::rpart(G::NPASS - 1, r) == 0) && dc_lane;
+        if (dc) {
+          buf[0] = make_float2(v[r].x, 0.0f);
+          buf[L] = make_float2(v[r].y, 0.0f);
+        } else {
+          buf[pa_inv(kl(r))] = v[r];  // kl holds pa(bin)
+        }
+      }
+      wave_sync();
+      if (valid) {
+        // complexSpectrum.js: the full N-point spectrum, X[N-k] = conj(X[k])
+        auto cr = gbl(ap->out.complex_real) + f * (uint64_t)N;
+        auto ci = gbl(ap->out.complex_imag) + f * (uint64_t)N;
+        for (int i = lane; i < N; i += 64) {
+          const float2 zz = i <= L ? buf[i] : buf[N - i];
+          cr[i] = zz.x;
+          ci[i] = i <= L ? zz.y : -zz.y;
+        }
+      }
+      wave_sync();
+    }
+    prio_hi<2>();
+#pragma unroll
+    for (int r = 0; r < R; ++r) amp[kl(r)] = ar[r];  // kl(r) = pa(bin)
+  }
+  wave_sync();
+
+  if (valid && ap->out.amplitude_spectrum) {
+    auto o = gbl(ap->out.amplitude_spectrum) + f * (uint64_t)L;
+#pragma unroll
+    for (int c = 0; c < R; ++c) o[c * 64 + lane] = amp[pa(c * 64 + lane)];
+  }
+  if (valid && ap->out.power_spectrum) {
+    auto o = gbl(ap->out.power_spectrum) + f * (uint64_t)L;
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      const float av = amp[pa(c * 64 + lane)];
+      o[c * 64 + lane] = av * av;  // powerSpectrum.js
+    }
+  }
+
+  // Per-frame reductions, lane t owns bins [R t, R t + R).
+  float av[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) av[jj] = amp[pa(R * lane + jj)];
+  prio_lo<2>();
+  prio_hi<64>();
+  MGX_MARK(amp_row_done);
+  // The moment and log sums only as far as a feature reads them (need_mom: 0 none, 1 S1 for
+  // centroid / slope, 2 S1..S4 and sum log2 a); the amplitude total T0 always (S0, rolloff,
+  // the non-finite test). SUB: a feature subset, the flags are read at run time; otherwise
+  // every feature is requested and the branches compile away (the all-feature kernel keeps
+  // its schedule: run-time branches there cost 0.7 %).
+  const int mom_level = SUB ? ap->need_mom : 2;
+  const bool need_mom = mom_level > 0, need_hi = mom_level > 1;
+  double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
+  float l2f = 0.0f;
+  if (need_hi) {
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) {
+      const double ad = av[jj];
+      T0 += ad;
+      if (jj > 0) {
+        T1 = __builtin_fma((double)jj, ad, T1);
+        T2 = __builtin_fma((double)(jj * jj), ad, T2);
+        T3 = __builtin_fma((double)(jj * jj * jj), ad, T3);
+        T4 = __builtin_fma((double)(jj * jj * jj * jj), ad, T4);
+      }
+    }
+    // sum log2 a by pairs, log2(a_j a_{j+1}) with the bare v_log_f32 (== log2f for normal
+    // inputs; one hardware log per two bins, and the product's rounding is ~2^-24 relative,
+    // finer than the log's own ulp). v_log_f32 flushes a denormal input to 0 (-inf): a wave
+    // whose sum is not finite (a zero, tiny, infinite or NaN amplitude, or a pair product
+    // leaving the normal range; rare) recomputes bin by bin with log2f's scaling.
+#pragma unroll
+    for (int jj = 0; jj < R; jj += 2) l2f += __builtin_amdgcn_logf(av[jj] * av[jj + 1]);
+    if (__ballot(!(__builtin_fabsf(l2f) < __builtin_huge_valf()))) {
+      l2f = 0.0f;
+#pragma unroll
+      for (int jj = 0; jj < R; ++jj) l2f += log2f(av[jj]);
+    }
+  } else if (need_mom) {
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) {
+      const double ad = av[jj];
+      T0 += ad;
+      if (jj > 0) T1 = __builtin_fma((double)jj, ad, T1);
+    }
+  } else {
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) T0 += (double)av[jj];
+  }
+  MGX_MARK(moments_done);
+  prio_hi<8>();
+  wave_sync();  // every lane has read the amplitude row: the buffer takes the prefix sums next
+  FrameRec& rec = recs[fb];
+  // Moments S1..S4 (bin-offset polynomial shift of the local partials) and sum log2 a:
+  // five sums over the lanes. Up to N = 1024 they go through one LDS transpose: lane l
+  // writes column l of a 5 x 64 table; after the prefix scan, lanes 0..39 each add 8
+  // entries (stride 8) of one row and 3 DPP steps finish the row in 8-lane groups; the
+  // table is read back at the end of the frame (after the mel sums). At N = 2048 (2 waves
+  // per SIMD) five DPP wave sums measured faster.
+  constexpr bool kMomLds = G::MOM_LDS;
+  constexpr int MS = G::MOM_STRIDE;
+  // P_p = sum_j (b + j)^p a_j = sum_m C(p, m) b^(p-m) T_m by a Taylor shift (c_i += b c_{i-1},
+  // four sweeps: 10 FMAs; every term is non-negative, so nothing cancels)
+  const double bb = (double)(R * lane);
+  double P1 = T1, P2 = T2, P3 = T3, P4 = T4;
+  if (need_hi) {
+    P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3); P2 = __builtin_fma(bb, P1, P2); P1 = __builtin_fma(bb, T0, P1);
+    P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3); P2 = __builtin_fma(bb, P1, P2);
+    P4 = __builtin_fma(bb, P3, P4); P3 = __builtin_fma(bb, P2, P3);
+    P4 = __builtin_fma(bb, P3, P4);
+  } else {
+    P1 = __builtin_fma(bb, T0, P1);
+  }
+  double* const momt = G::MOM_SLOT ? pbuf : mom;
+  if (kMomLds && need_mom) {
+    momt[0 * MS + lane] = P1;
+    if (need_hi) {
+      momt[1 * MS + lane] = P2;
+      momt[2 * MS + lane] = P3;
+      momt[3 * MS + lane] = P4;
+      momt[4 * MS + lane] = (double)l2f;
+    }
+  }
+  // prefix P(k) = sum_{i<k} a_i: lane-exclusive offset + local prefix
+  const double incl = wave_inclusive_scan(T0);
+  const double excl = dpp_d<0x138>(incl);  // wave_shr:1 (lane 0 reads 0)
+  const double total = readlane_d(incl, 63);
+  // the moment transpose's reduction (lanes 0..39: 8 entries of one row, then 3 DPP steps)
+  auto mom_reduce = [&]() {
+    const int row = lane < 40 ? lane >> 3 : 0;
+    const double* src = momt + row * MS + (lane & 7);  // entries g, g+8, ..., g+56 of the row
+    double t = ((src[0] + src[8]) + (src[16] + src[24])) + ((src[32] + src[40]) + (src[48] + src[56]));
+    t += dpp_d<0xB1>(t);   // quad_perm [1,0,3,2]
+    t += dpp_d<0x4E>(t);   // quad_perm [2,3,0,1]
+    t += dpp_d<0x141>(t);  // row_half_mirror: each 8-lane group holds its row's total
+    if (lane < 40 && (lane & 7) == 0) (&rec.S[1])[row] = t;  // S[1..4], then ln2sum
+  };
+  if (G::MOM_SLOT && need_mom) {
+    wave_sync();
+    mom_reduce();
+    wave_sync();  // the table's reads are done: the buffer takes the prefix row
+  }
+  // spectralRolloff.js:6-15: the largest m with P(m) <= 0.99 total (P(0) = 0).
+  const double thr = 0.99 * total;
+  int cnt = 0;
+  const bool need_prefix = opaque(0);
+  if (need_prefix) {
+    double pk = excl;  // P(R lane + jj), accumulated again rather than kept (registers)
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) {
+      pbuf[pd(R * lane + jj)] = pk;
+      cnt += __popcll(__ballot(pk <= thr));
+      pk += (double)av[jj];
+    }
+  }
+  const int roll_m = (total > thr) ? cnt - 1 : L;
+  MGX_MARK(prefix_done);
+  // The lane's mel records, then (G::PF == 2) the next frame: issued after the last table
+  // load this frame waits on before them, so no wait of this frame is held up by the
+  // prefetch; the band and mel sums, the moment finish and phase 2 run while it is in
+  // flight. (Issued any earlier, the extra live registers spill around the moment sums,
+  // and a spill reload is a vector-memory wait behind the prefetch.)
+  MelTab<N> mt;
+  if (ap->need_mfcc) mt.load(ap, lane);
+  prefetch_next();
+  if (!kMomLds && need_mom) {
+    const double S1 = wave_sum(P1);
+    double S2 = 0, S3 = 0, S4 = 0, l2 = 0;
+    if (need_hi) {
+      S2 = wave_sum(P2); S3 = wave_sum(P3); S4 = wave_sum(P4);
+      l2 = wave_sum((double)l2f);
+    }
+    wave_sync();
+    if (lane == 0) {
+      rec.S[1] = S1; rec.S[2] = S2; rec.S[3] = S3; rec.S[4] = S4;
+      rec.ln2sum = l2;
+    }
+  }
+  MGX_MARK(prefetch_issued);
+  if (need_prefix && lane < kBark) {
+    const int lb = opaque(lane);  // (an address kept live across the frame loop spills at N = 2048)
+    rec.band[lb] = pbuf[pd(klim[lb + 1])] - pbuf[pd(klim[lb])];  // limits staged in LDS
+  }
+  if (lane == 0) {
+    rec.S[0] = total;
+    rec.roll_m = roll_m;
+  }
+  // A non-finite amplitude (Inf/NaN samples, or overflow in the FFT) breaks the prefix
+  // differences (Inf - Inf) and the segment decomposition of the mel sums (the reference's
+  // zero weights turn Inf into NaN in every band). Such frames — wave-uniform, rare — take
+  // the reference's own summation: bark bands bin by bin in double (loudness.js:47-66),
+  // mel bands over all bins in reference order (mfcc.js:53-62).
+  // (total = sum of the amplitudes in double: non-finite iff some amplitude is.)
+  MGX_MARK(bands_done);
+  if (!(total < __builtin_huge_val())) {
+    nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
+  } else if (SUB && ap->need_mfcc && ap->mfcc_reference) {  // (the all-feature kernel never has the flag)
+    mel_reference_order<N>(ap, av, lane, buf, rec);
+  } else if (ap->need_mfcc) {
+    mel_energies<N>(ap, av, lane, buf, rec, mt);
+  }
+  MGX_MARK(mel_done);
+  if (kMomLds && !G::MOM_SLOT && need_mom) {
+    wave_sync();
+    mom_reduce();
+  }
+  prio_lo<8>();
+  MGX_MARK(frame_end);
+  wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
+}
+
+// mfcc.js:85-93: coefficient c of one frame, sum_n dct[c][n] * lm[n] in double, in the
+// reference's sequential order. The product of two floats is exact in double, so an FMA
+// equals the reference's multiply-then-add. lm and the LDS table are zero-padded to a
+// multiple of 8 bands (0 * 0 adds nothing), so groups of 8 loads issue together.
+__device__ __forceinline__ double dct_sum(const float* dct, const float* lm, int c, int nc, int nfilt) {
+  double v = 0.0;
+  for (int n0 = 0; n0 < nfilt; n0 += 8) {
+    float dv[8], lv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      dv[u] = dct[c + (n0 + u) * nc];
+      lv[u] = lm[n0 + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v = __builtin_fma((double)dv[u], (double)lv[u], v);
+  }
+  return v;
+}
+
+// 2^y in double for the geometric mean of spectralFlatness.js: 2^floor(y) * 2^frac(y) with
+// the f32 hardware exp2 on [0, 1) (relative error ~1.5e-7, against the 1e-5 bar).
+__device__ __forceinline__ double exp2_mean(double y) {
+  // -inf (a zero amplitude) -> 0, +inf -> inf, NaN -> NaN; v_ldexp_f64 saturates to 0 / inf
+  // for any exponent the int conversion holds
+  if (!(__builtin_fabs(y) < 1e9)) return y != y ? y : y > 0.0 ? __builtin_huge_val() : 0.0;
+  const double n = floor(y);
+  return ldexp((double)__builtin_amdgcn_exp2f((float)(y - n)), (int)n);
+}
+
+// sqrt(x) from the hardware reciprocal square root and one Newton step (relative error
+// ~1e-15) instead of the IEEE square-root sequence; 0, +inf and negative/NaN inputs give
+// sqrt's own values (0, inf, NaN).
+__device__ __forceinline__ double sqrt_d(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  const double g = x * y, h = 0.5 * y;
+  const double r = __builtin_fma(-h, g, 0.5);
+  const double s = __builtin_fma(g, r, g);
+  return (x > 0.0 && x < __builtin_huge_val()) ? s : (x == 0.0 || x == __builtin_huge_val()) ? x : __builtin_nan("");
+}
+
+// 1/x from the hardware reciprocal and one Newton step (relative error ~1e-16, against the
+// 1e-5 bar) instead of the IEEE division sequence; 0, +-inf and NaN keep the raw reciprocal's
+// IEEE values (inf, 0, NaN), where the Newton step would turn them into NaN.
+__device__ __forceinline__ double rcp_d(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  const double e = __builtin_fma(-x, r, 1.0);
+  return __builtin_fabs(e) < 1.0 ? __builtin_fma(r, e, r) : r;
+}
+
+// One of the ten spectral/time scalars of a frame from its phase-1 record, formulas as
+// written in the reference extractors. Branch-free: every lane evaluates the shared terms
+// (moments, spread) and selects its feature's numerator and denominator, so a wave
+// holding ten different features runs one instruction stream.
+template <int N>
+__device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int sc) {
+  constexpr int L = N / 2;
+  const double S0 = rc.S[0];
+  // utils.js:1-11 mu(p) = sum k^p a_k / sum a_k: one reciprocal and four products (S0 is
+  // 0, >= 2^-149 or non-finite, so 1/S0 neither overflows nor hides a NaN of the quotient)
+  const double inv = rcp_d(S0);
+  const double m1 = rc.S[1] * inv, m2 = rc.S[2] * inv, m3 = rc.S[3] * inv, m4 = rc.S[4] * inv;
+  const double sd = sqrt_d(m2 - m1 * m1);  // spectralSpread.js
+  double num, den = 1.0;
+  switch (sc) {  // selects only (no divergent code: every case is a few operands)
+    case MGX_RMS: num = rc.energy * (1.0 / N); break;  // rms.js: sqrt(sum / N), N a power of 2
+    case MGX_ENERGY: num = rc.energy; break;           // energy.js
+    case MGX_ZCR: num = (double)rc.zcr; break;         // zcr.js
+    case MGX_SPECTRAL_CENTROID: num = m1; break;       // spectralCentroid.js
+    case MGX_SPECTRAL_FLATNESS:                        // spectralFlatness.js: geometric / arithmetic mean
+      num = exp2_mean(rc.ln2sum * (1.0 / L)) * L;
+      den = S0;
+      break;
+    case MGX_SPECTRAL_SLOPE:                           // spectralSlope.js:9-21
+      num = L * ((q->sample_rate / N) * rc.S[1]) - q->freq_sum * S0;
+      den = S0 * (q->pow_freq_sum - q->freq_sum * q->freq_sum);
+      break;
+    case MGX_SPECTRAL_ROLLOFF: num = (double)rc.roll_m * q->nyq_bin; break;  // spectralRolloff.js:6-15
+    case MGX_SPECTRAL_SPREAD: num = sd; break;
+    case MGX_SPECTRAL_SKEWNESS:                        // spectralSkewness.js
+      num = 2.0 * m1 * m1 * m1 - 3.0 * m1 * m2 + m3;
+      den = sd * sd * sd;
+      break;
+    default:                                           // spectralKurtosis.js (6 mu1 mu2 as written)
+      num = -3.0 * m1 * m1 * m1 * m1 + 6.0 * m1 * m2 - 4.0 * m1 * m3 + m4;
+      den = sd * sd * sd * sd;
+      break;
+  }
+  const double v = num * rcp_d(den);
+  return sc == MGX_RMS ? sqrt_d(v) : v;
+}
+
+template <int N, bool FAITH, bool LITERAL, bool SUB>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
+  using G = Geo<N>;
+  using PG = PassGeo<N>;
+  using LY = Lds<N>;
+  constexpr int R = G::R, CH = G::CH, FPW = G::FPW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
+  float* dct_lds = reinterpret_cast<float*>(smem + LY::dct_off);
+  double* mom = G::MOM_SLOT ? nullptr : reinterpret_cast<double*>(smem + LY::mom_off) + (threadIdx.x >> 6) * (5 * G::MOM_STRIDE);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float2* buf = slot_all + wave * G::SLOT_PHYS;
+  FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off) + wave * FPW;  // this wave's records
+  KArgs* ap = args_ptr();
+
+  // Kernel constants and the DCT table, once per workgroup (the only workgroup barrier).
+  {
+    void** kptr = reinterpret_cast<void**>(smem + LY::kc_off);
+    int* klim = reinterpret_cast<int*>(smem + LY::kc_off + 16 * 8);
+    if (threadIdx.x < MGX_NUM_SCALARS) kptr[threadIdx.x] = ap->out.scalars[threadIdx.x];
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = gbl(ap->t.bblim)[threadIdx.x - 64];
+  }
+  if constexpr (G::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
+    double2* twl = reinterpret_cast<double2*>(smem + LY::twl_off);
+    const GTw tw = gbl(ap->t.tw), twm = gbl(ap->t.twm);
+    auto stage_copy = [&](auto P_, auto I_) {
+      constexpr int P = decltype(P_)::value, I = decltype(I_)::value;
+      constexpr int q0 = PG::q0(P), mask = (1 << (q0 + I)) - 1;
+      for (int i = threadIdx.x; i < TwLds<N>::mixed_n(P); i += kThreads)
+        twl[TwLds<N>::off(P, I, false) + i] = ld_tw(twm, 2 * mask + i);  // entries mask + la, la < 2^q0
+      for (int i = threadIdx.x; i < TwLds<N>::gen_n(P, I); i += kThreads)
+        twl[TwLds<N>::off(P, I, true) + i] = ld_tw(tw, mask + (1 << q0) + i);
+      if (threadIdx.x == 0) twl[TwLds<N>::fw_off(P, I)] = ld_tw(twm, 2 * (G::L - 1 + q0 + I));
+    };
+    static_assert(G::NPASS == 3 && PG::m(1) == 3 && PG::m(2) == 3, "TwLds: the N = 1024 pass structure");
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    using C2 = std::integral_constant<int, 2>;
+    stage_copy(C1{}, C0{}); stage_copy(C1{}, C1{}); stage_copy(C1{}, C2{});
+    stage_copy(C2{}, C0{}); stage_copy(C2{}, C1{}); stage_copy(C2{}, C2{});
+  }
+  if (ap->need_spectrum && ap->need_mfcc) {
+    const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
+    const auto dct = gbl(ap->t.dct);
+    for (int i = threadIdx.x; i < ntp; i += kThreads) dct_lds[i] = i < nt ? dct[i] : 0.0f;
+  }
+  lds_barrier();
+
+  int lp[G::NPASS];
+#pragma unroll
+  for (int p = 0; p < G::NPASS; ++p) lp[p] = PG::lanepart(p, lane);
+  KlTab<N> kl;  // spectrum bin held by each register after the last pass
+  {
+    const auto klist = gbl(ap->t.klist);
+#pragma unroll
+    for (int r = 0; r < R; ++r) kl.set(r, pa(klist[lp[G::NPASS - 1] | PG::rpart(G::NPASS - 1, r)]));
+  }
+  const bool dc_lane = lp[G::NPASS - 1] == 0;
+
+  // Every wave works through its own batches of FPW consecutive frames: phase 1 per
+  // frame, then phase 2 over the batch, with wave-level synchronisation only.
+  const uint64_t nf = ap->num_frames;
+  const uint64_t nb = (nf + FPW - 1) / FPW;
+  // Each workgroup owns one contiguous range of batches, its 4 waves interleaved
+  // (wave w takes batches 4k + w), so the 16 frames the waves finish together are
+  // consecutive: a workgroup fills whole 64/128-byte lines of every scalar output in its
+  // own XCD's L2 instead of sharing each line with a workgroup on another XCD.
+  const uint64_t wstride = 4;
+  const uint64_t ng = (nb + 3) / 4, per = (ng + gridDim.x - 1) / gridDim.x;
+  const uint64_t g0 = (uint64_t)blockIdx.x * per, g1 = g0 + per < ng ? g0 + per : ng;
+  const uint64_t b0 = g0 * 4 + wave, bend = g1 * 4 < nb ? g1 * 4 : nb;
+  // Loads are unconditional (the frame index is clamped; results of frames past the end
+  // are never stored), so they issue back to back with no branches or waits between them.
+  // With G::PREFETCH the next frame of the wave is loaded while this one is processed.
+  auto frame_ptr = [&](uint64_t b, int j) {
+    uint64_t f = b * FPW + j;
+    f = f < nf ? f : nf - 1;
+    return (GF)(gbl(args_ptr()->frames) + f * (uint64_t)N + lane);
+  };
+  auto load = [&](float (&xv)[CH], uint64_t b, int j) {
+    const GF xin = frame_ptr(b, j);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) xv[c] = ld_frame(xin + c * 64);
+  };
+
+  float wreg[CH];
+  if constexpr (G::WIN_REG) {
+    const GF w = gbl(ap->t.window);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) wreg[c] = w[c * 64 + lane];
+  }
+  float xn[G::PREFETCH ? CH : 1];
+  if constexpr (G::PREFETCH) load(xn, b0, 0);
+
+  for (uint64_t b = b0; b < bend; b += wstride) {
+    const uint64_t f0 = b * FPW;
+    // ------------------------------------------------------------- phase 1
+    for (int j = 0; j < FPW; ++j) {
+      const uint64_t f = f0 + j;
+      float x[CH];
+      GF next = nullptr;
+      if constexpr (G::PF == 1) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) x[c] = xn[c];
+        if (j + 1 < FPW) load(xn, b, j + 1);
+        else load(xn, b + wstride, 0);
+      } else if constexpr (G::PF == 2) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) x[c] = xn[c];
+        next = frame_ptr(j + 1 < FPW ? b : b + wstride, j + 1 < FPW ? j + 1 : 0);
+      } else {
+        load(x, b, j);
+      }
+      frame_phase1<N, FAITH, LITERAL, SUB>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
+                                      reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
+                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg);
+    }
+    wave_sync();
+
+    // ------------------------------------------------------------- phase 2
+    // Lane ids and the argument pointer are re-derived so that nothing phase 2 needs is
+    // hoisted out of the batch loop (it would stay live across the FFT).
+    MGX_MARK(phase2_start);
+    prio_hi<4>();
+    {
+      KArgs* q = args_ptr();
+      const int l2 = opaque(lane);
+      if (q->need_spectrum && q->need_loudness) {
+        // 32 lanes per frame (24 bands + 8 idle), so a frame's reductions stay in two DPP rows.
+#pragma unroll
+        for (int i0 = 0; i0 < FPW * 32; i0 += 64) {
+          const int i = i0 + l2;
+          const int fb = i >> 5, bnd = i & 31;
+          const uint64_t f = f0 + fb;
+          const bool live = bnd < kBark;
+          const double sum = recs[fb].band[live ? bnd : 0];
+          // loudness.js:62 Math.pow(sum, 0.23), stored to Float32Array
+          float sp = pow023(sum);
+          if (!live) sp = 0.0f;
+          if (live && f < q->num_frames && q->out.loudness_specific) gbl(q->out.loudness_specific)[f * kBark + bnd] = sp;
+          // loudness.js:67-69 total; perceptualSpread.js:7-12 max; perceptualSharpness.js:7-14
+          // (off-by-one spec[i+1] for i < 15, then the constant 0.066 e^{0.171 (i+1)} tail).
+          // total in double (perceptualSpread's (total - max) cancels); max exact in float32;
+          // the sharpness weighted sum in float32 (a plain sum of positive terms).
+          double tot = sp;
+          float mx = sp, sh = (bnd >= 1 && bnd <= 15) ? (float)bnd * sp : 0.0f;
+          tot += dpp_d<0xB1>(tot); mx = fmaxf(mx, dpp_f<0xB1>(mx)); sh += dpp_f<0xB1>(sh);
+          tot += dpp_d<0x4E>(tot); mx = fmaxf(mx, dpp_f<0x4E>(mx)); sh += dpp_f<0x4E>(sh);
+          tot += dpp_d<0x141>(tot); mx = fmaxf(mx, dpp_f<0x141>(mx)); sh += dpp_f<0x141>(sh);
+          tot += dpp_d<0x140>(tot); mx = fmaxf(mx, dpp_f<0x140>(mx)); sh += dpp_f<0x140>(sh);
+          // rows 2r and 2r+1 hold one frame: row_bcast:15 adds row 2r's total into row 2r+1
+          tot += dpp_d<0x142, 0xA>(tot); mx = fmaxf(mx, dpp_f<0x142, 0xA>(mx)); sh += dpp_f<0x142, 0xA>(sh);
+          if (bnd == 31 && f < q->num_frames) {
+            const double rt = rcp_d(tot);  // one reciprocal for both quotients
+            const double ps = (tot - (double)mx) * rt;
+            const double sv[3] = {tot, ps * ps, ((double)sh + q->sharp_tail_sum) * (0.11 * rt)};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              void* dst = q->out.scalars[MGX_LOUDNESS_TOTAL + k];
+              if (!dst) continue;
+              if (q->scalar_f64) gbl(static_cast<double*>(dst))[f] = sv[k];
+              else gbl(static_cast<float*>(dst))[f] = (float)sv[k];
+            }
+          }
+        }
+      }
+      MGX_MARK(loud2_done);
+      if (q->need_spectrum && q->need_mfcc) {
+        // mfcc.js:64 Math.log of the band energies, stored to Float32Array
+        const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
+        const bool ref_log = SUB && q->mfcc_reference;  // the double Math.log, then float32
+        for (int i = l2; i < FPW * nfp; i += 64) {
+          const int band = i / FPW, fb = i % FPW;
+          recs[fb].lm[band] = band < nfilt ? (ref_log ? (float)log((double)recs[fb].lm[band]) : ln_f32(recs[fb].lm[band]))
+                                           : 0.0f;  // padding for dct_sum
+        }
+      }
+    }
+    wave_sync();
+    {
+      KArgs* q = args_ptr();
+      const int l2 = opaque(lane);
+      MGX_MARK(ln_done);
+      if (q->need_spectrum && q->need_mfcc) {
+        const int nc = q->ncoef, nfilt = q->nfilt;
+        if (q->dct_sequential || (SUB && q->mfcc_reference)) {
+        // MGX_FLAG_DCT_SEQUENTIAL: VALU FMAs in the reference's sequential order, one lane per
+        // (coefficient, frame). (The matrix-core form below is the default: 0.5 % faster for the
+        // whole kernel and equal on every golden coefficient)
+        for (int i = l2; i < FPW * nc; i += 64) {
+          const int c = i / FPW, fb = i % FPW;
+          const uint64_t f = f0 + fb;
+          const double v = dct_sum(dct_lds, recs[fb].lm, c, nc, nfilt);
+          if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(v / nc);
+        }
+        } else {
+        // mfcc.js:85-93 on the FP64 matrix cores, v_mfma_f64_4x4x4_4b_f64: 4 blocks of a
+        // 4 x 4 x 4 product per instruction. Block g holds coefficients 4g..4g+3 of a
+        // 16-coefficient tile against the batch's 4 frames; a step covers 4 bands. Lane layout
+        // (measured, tools/ubench/mfma_f64_4x4_layout.hip): A[i][k] of block g at lane
+        // 16k + 4g + i, B[k][j] at 16k + 4g + j, D[i][j] at 16i + 4g + j. So lane l loads
+        // DCT[c = l & 15][band n0 + (l >> 4)] and lm[frame l & 3][band n0 + (l >> 4)], and ends
+        // with coefficient 4 ((l >> 2) & 3) + (l >> 4) of frame l & 3. The products of two
+        // floats are exact in double, as in the reference; only the f64 summation order differs.
+        static_assert(FPW == 4, "one 4 x 4 block column per frame of the batch");
+        const int kk = l2 >> 4, fa = l2 & 3, nsteps = (nfilt + 3) >> 2;
+        const float* lmrow = recs[fa].lm;
+        for (int mt = 0; mt < nc; mt += 16) {
+          const int ca = mt + (l2 & 15);
+          double acc = 0.0;
+          for (int st = 0; st < nsteps; ++st) {
+            const int n = 4 * st + kk;  // < nfilt rounded up to 8: the tables are zero-padded
+            const float av = ca < nc ? dct_lds[ca + n * nc] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)av, (double)lmrow[n], acc, 0, 0, 0);
+          }
+          const int c = mt + 4 * ((l2 >> 2) & 3) + kk;
+          const uint64_t f = f0 + fa;
+          if (c < nc && f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(acc / nc);
+        }
+        }
+      }
+      MGX_MARK(dct_done);
+      // the other scalar features: one lane per (feature, frame)
+      for (int i = l2; i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {
+        const int sc = i / FPW, fb = i % FPW;
+        const uint64_t f = f0 + fb;
+        void* dst = reinterpret_cast<void* const*>(smem + LY::kc_off)[sc];
+        if (f >= q->num_frames || dst == nullptr) continue;
+        const double v = scalar_value<N>(q, recs[fb], sc);
+        if (q->scalar_f64) gbl(static_cast<double*>(dst))[f] = v;
+        else gbl(static_cast<float*>(dst))[f] = (float)v;
+      }
+    }
+    prio_lo<4>();
+    MGX_MARK(phase2_end);
+    wave_sync();  // records and slot buffer are reused by the next batch
+  }
+}
+
+__global__ void synth_kernel(float* __restrict__ out, uint64_t count, uint64_t seed, uint64_t first) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < count; i += stride) {
+    float r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      uint64_t z = seed + (first + i + u + 1) * 0x9E3779B97F4A7C15ull;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      r[u] = (float)(uint32_t)(z >> 40) * 0x1p-23f - 1.0f;
+    }
+    if (i + 3 < count && ((reinterpret_cast<uintptr_t>(out + i) & 15) == 0)) {
+      *reinterpret_cast<float4*>(out + i) = make_float4(r[0], r[1], r[2], r[3]);
+    } else {
+      for (int u = 0; u < 4 && i + u < count; ++u) out[i + u] = r[u];
+    }
+  }
+}
+
+// PCM -> float32 of one channel, decodeAudioData's scaling (include/meyda_gpu.h).
+__global__ void pcm_decode_kernel(const unsigned char* __restrict__ pcm, uint64_t count, uint32_t format,
+                                  uint32_t stride, uint32_t offset, float* __restrict__ out) {
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += step) {
+    // samples are assembled from bytes: a caller's device pointer need not be aligned
+    const unsigned char* b = pcm + i * stride + offset;
+    auto w32 = [b]() { return (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24; };
+    float v;
+    switch (format) {
+      case MGX_PCM_S16: v = (float)(int16_t)(uint16_t)((uint32_t)b[0] | (uint32_t)b[1] << 8) * (1.0f / 32768.0f); break;
+      case MGX_PCM_U8: v = (float)((int)b[0] - 128) * (1.0f / 128.0f); break;
+      case MGX_PCM_S24: {
+        const int32_t u = (int32_t)((uint32_t)b[0] << 8 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 24) >> 8;
+        v = (float)u * (1.0f / 8388608.0f);
+        break;
+      }
+      case MGX_PCM_S32: v = (float)((double)(int32_t)w32() * (1.0 / 2147483648.0)); break;
+      default: v = __builtin_bit_cast(float, w32()); break;
+    }
+    out[i] = v;
+  }
+}
+
+// Packed transfer buffer -> the root's structure-of-arrays outputs (group.cpp). One
+// workgroup row per segment (blockIdx.y); dword copies: every field is a whole number of
+// dwords per frame, and a shard's destination offset is only dword-aligned.
+__global__ void unpack_kernel(UnpackArgs a) {
+  const int s = blockIdx.y;
+  if (s >= a.nseg) return;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(a.src + a.src_off[s]);
+  uint32_t* dst = static_cast<uint32_t*>(a.dst[s]);
+  const uint64_t n = a.dwords[s];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+template <int N, bool FAITH, bool LITERAL, bool SUB = false>
+hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
+  const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
+  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB>), dim3(grid), dim3(kThreads), lds, stream, a);
+  return hipGetLastError();
+}
+
+template <int N, bool FAITH, bool LITERAL, bool SUB = false>
+int occupancy_n(size_t lds) {
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL, SUB>, kThreads, lds) !=
+      hipSuccess)
+    return 0;
+  return blocks;
+}
+
+template <int N>
+int occupancy_prec(int precision, int mode, int ncoef, int nfilt) {
+  const size_t lds = Lds<N>::bytes(ncoef, nfilt);
+  if (mode == MGX_MODE_LITERAL) return occupancy_n<N, true, true>(lds);
+  if (precision == MGX_PRECISION_FAST) return occupancy_n<N, false, false>(lds);
+  // the grid serves both faithful kernels (all features / a subset)
+  const int a = occupancy_n<N, true, false>(lds), b = occupancy_n<N, true, false, true>(lds);
+  return a < b ? a : b;
+}
+
+template <int N>
+hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, hipStream_t stream) {
+  if (mode == MGX_MODE_LITERAL) return launch_n<N, true, true>(a, grid, stream);
+  if (precision == MGX_PRECISION_FAST) return launch_n<N, false, false>(a, grid, stream);
+  // a spectral feature subset that skips the moment / prefix work takes the SUB kernel
+  // (and so does MGX_FLAG_MFCC_REFERENCE: the all-feature kernel keeps its schedule)
+  if (a.need_spectrum && (!(a.need_mom == 2 && a.need_prefix) || a.mfcc_reference))
+    return launch_n<N, true, false, true>(a, grid, stream);
+  return launch_n<N, true, false>(a, grid, stream);
+}
+
+}  // namespace
+
+size_t extract_lds_bytes(int n, int ncoef, int nfilt) {
+  switch (n) {
+    case 256: return Lds<256>::bytes(ncoef, nfilt);
+    case 512: return Lds<512>::bytes(ncoef, nfilt);
+    case 1024: return Lds<1024>::bytes(ncoef, nfilt);
+    case 2048: return Lds<2048>::bytes(ncoef, nfilt);
+    default: return 0;
+  }
+}
+
+int frames_per_batch(int n) {
+  switch (n) {
+    case 256: return Geo<256>::FB;
+    case 512: return Geo<512>::FB;
+    case 1024: return Geo<1024>::FB;
+    case 2048: return Geo<2048>::FB;
+    default: return 0;
+  }
+}
+
+int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt) {
+  switch (n) {
+    case 256: return occupancy_prec<256>(precision, mode, ncoef, nfilt);
+    case 512: return occupancy_prec<512>(precision, mode, ncoef, nfilt);
+    case 1024: return occupancy_prec<1024>(precision, mode, ncoef, nfilt);
+    case 2048: return occupancy_prec<2048>(precision, mode, ncoef, nfilt);
+    default: return 0;
+  }
+}
+
+hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, int grid,
+                          hipStream_t stream) {
+  switch (n) {
+    case 256: return launch_prec<256>(precision, mode, a, grid, stream);
+    case 512: return launch_prec<512>(precision, mode, a, grid, stream);
+    case 1024: return launch_prec<1024>(precision, mode, a, grid, stream);
+    case 2048: return launch_prec<2048>(precision, mode, a, grid, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_pcm_decode(const void* pcm, uint64_t count, uint32_t format, uint32_t channels,
+                             uint32_t channel, float* out, hipStream_t stream) {
+  const uint32_t bps = format == MGX_PCM_S16 ? 2 : format == MGX_PCM_U8 ? 1 : format == MGX_PCM_S24 ? 3 : 4;
+  uint64_t blocks = (count + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(pcm_decode_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     static_cast<const unsigned char*>(pcm), count, format, bps * channels, bps * channel, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack(const UnpackArgs& a, hipStream_t stream) {
+  uint64_t most = 0;
+  for (int i = 0; i < a.nseg; ++i) most = a.dwords[i] > most ? a.dwords[i] : most;
+  if (a.nseg == 0 || most == 0) return hipSuccess;
+  uint64_t bx = (most + 1023) / 1024;
+  if (bx > 256) bx = 256;
+  hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)bx, (unsigned)a.nseg), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t first_index,
+                        hipStream_t stream) {
+  const uint64_t threads = (count + 3) / 4;
+  uint64_t blocks = (threads + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, out, count, seed, first_index);
+  return hipGetLastError();
+}
+
+}  // namespace mgx

@@ -14,8 +14,8 @@ SRC = os.path.join(ROOT, "meyda_amd", "csrc")
 
 # name -> list of (anchor, replacement); opaque(0) keeps the skipped code compiled but never run
 PATCHES = {
-    "no_phase2": [("    MGX_MARK(phase2_start);\n    {", "    MGX_MARK(phase2_start);\n    if (opaque(0)) {\n    {"),
-                  ("    MGX_MARK(phase2_end);", "    }\n    MGX_MARK(phase2_end);")],
+    "no_phase2": [("    MGX_MARK(phase2_start);\n    prio_hi<4>();\n    {", "    MGX_MARK(phase2_start);\n    prio_hi<4>();\n    if (opaque(0)) {\n    {"),
+                  ("    prio_lo<4>();\n    MGX_MARK(phase2_end);", "    }\n    prio_lo<4>();\n    MGX_MARK(phase2_end);")],
     "no_loud2": [("if (q->need_spectrum && q->need_loudness) {", "if (opaque(0) && q->need_spectrum && q->need_loudness) {")],
     "no_ln": [("if (q->need_spectrum && q->need_mfcc) {\n        // mfcc.js:64",
                "if (opaque(0) && q->need_spectrum && q->need_mfcc) {\n        // mfcc.js:64")],
