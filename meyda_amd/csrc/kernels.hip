@@ -123,7 +123,10 @@ struct Geo {
 #ifndef MGX_TW_LDS
 #define MGX_TW_LDS 1
 #endif
-  static constexpr bool TW_LDS = MGX_TW_LDS && N == 1024 && MOM_SLOT;
+#ifndef MGX_TW_LDS2048
+#define MGX_TW_LDS2048 1
+#endif
+  static constexpr bool TW_LDS = MGX_TW_LDS && ((N == 1024 && MOM_SLOT) || (N == 2048 && MGX_TW_LDS2048));
   // Register prefetch of the next frame. A vector-memory wait is in issue order (vmcnt),
   // so a table load a frame waits on (window, twiddles) also waits for a prefetch issued
   // before it: prefetching at the start of the frame made every frame wait for the next
@@ -198,15 +201,22 @@ struct PassGeo {
 
 
 // LDS image of the tame passes' per-lane twiddles (Geo<N>::TW_LDS), in double2 entries. In
-// pass P >= 1 at N = 1024 the location bits below the pass are lane bits [0, q0) and the
-// stage bits below stage q are register bits [q0, q): the mixed pairs of stage q read entries
-// mask + la, la < 2^q0 (two double2 each: (b, c0), (t4, kL)), the generic ones mask + (la | rp),
-// rp != 0, i.e. [mask + 2^q0, mask + 2^q). Per (P, I): the mixed block, then the generic one.
+// pass P >= 1 the location bits below the pass's first stage bit q0 that are lane bits are the
+// lowest nl = min(q0, 6) (the lanes take the lowest free bits), and every bit in [nl, q) below
+// stage q is a register bit (the stage bits [q0, q), at N = 2048 also the leftover register
+// bits [6, 8) of the last pass). So the mixed pairs of stage q read mixed-table entries
+// mask + la, la < 2^nl (two double2 each: (b, c0), (t4, kL)), and the generic ones
+// mask + (la | rp), rp != 0: the contiguous [mask + 2^nl, mask + 2^q). Per (P, I): the mixed
+// block, then the generic one. At N = 2048 only pass 1 is staged (pass_lds: 4.9 KB; with the
+// last pass's mixed entries too, 9 KB, the workgroup no longer fit 3 per CU and the launch ran
+// 20 % slower); the last pass reads its twiddles from global memory as before.
 template <int N>
 struct TwLds {
   using PG = PassGeo<N>;
-  static constexpr int mixed_n(int P) { return 2 << PG::q0(P); }
-  static constexpr int gen_n(int P, int I) { return (1 << (PG::q0(P) + I)) - (1 << PG::q0(P)); }
+  static constexpr int nl(int P) { return PG::q0(P) < 6 ? PG::q0(P) : 6; }
+  static constexpr bool pass_lds(int P) { return !(N == 2048 && P == 2); }
+  static constexpr int mixed_n(int P) { return pass_lds(P) ? 2 << nl(P) : 0; }
+  static constexpr int gen_n(int P, int I) { return pass_lds(P) ? (1 << (PG::q0(P) + I)) - (1 << nl(P)) : 0; }
   static constexpr int off(int P, int I, bool gen) {
     int o = 0;
     for (int p = 1; p < Geo<N>::NPASS; ++p)
@@ -223,7 +233,7 @@ struct TwLds {
     for (int p = 1; p < Geo<N>::NPASS; ++p)
       for (int i = 0; i < PG::m(p); ++i) {
         if (p == P && i == I) return o;
-        ++o;
+        if (pass_lds(p)) ++o;
       }
     return o;
   }
@@ -504,7 +514,7 @@ __device__ __forceinline__ void bfly_mixed_tame(float2& lo, float2& hi, double2 
 template <int N, int P, int I, bool FAITH, bool TAME>
 __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm,
                                           const double2* twl) {
-  constexpr bool LT = FAITH && TAME && Geo<N>::TW_LDS && P > 0;  // twiddles from the LDS image
+  constexpr bool LT = FAITH && TAME && Geo<N>::TW_LDS && P > 0 && TwLds<N>::pass_lds(P);  // twiddles from the LDS image
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int q = PG::q0(P) + I;
@@ -538,7 +548,7 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
       }
       else bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, fidx, la == 0);
     } else if constexpr (LT) {
-      bfly_generic_c(v[r], v[hi], twl[TwLds<N>::off(P, I, true) + ((la | rp) - (1 << PassGeo<N>::q0(P)))]);
+      bfly_generic_c(v[r], v[hi], twl[TwLds<N>::off(P, I, true) + ((la | rp) - (1 << TwLds<N>::nl(P)))]);
     } else {
       bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + (la | rp));
     }
@@ -1446,6 +1456,25 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   return sc == MGX_RMS ? sqrt_d(v) : v;
 }
 
+// Copy of the TwLds image from the plan tables, once per workgroup (before its LDS barrier).
+template <int N, int P, int I>
+__device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
+  if constexpr (P < Geo<N>::NPASS) {
+    if constexpr (I < PassGeo<N>::m(P)) {
+      using T = TwLds<N>;
+      constexpr int mask = (1 << (PassGeo<N>::q0(P) + I)) - 1;
+      for (int i = threadIdx.x; i < T::mixed_n(P); i += kThreads)
+        twl[T::off(P, I, false) + i] = ld_tw(twm, 2 * mask + i);  // entries mask + la, la < 2^nl
+      for (int i = threadIdx.x; i < T::gen_n(P, I); i += kThreads)
+        twl[T::off(P, I, true) + i] = ld_tw(tw, mask + (1 << T::nl(P)) + i);
+      if (T::pass_lds(P) && threadIdx.x == 0) twl[T::fw_off(P, I)] = ld_tw(twm, 2 * (Geo<N>::L - 1 + PassGeo<N>::q0(P) + I));
+      stage_twiddles<N, P, I + 1>(twl, tw, twm);
+    } else {
+      stage_twiddles<N, P + 1, 0>(twl, tw, twm);
+    }
+  }
+}
+
 template <int N, bool FAITH, bool LITERAL, bool SUB>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
@@ -1471,23 +1500,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = gbl(ap->t.bblim)[threadIdx.x - 64];
   }
   if constexpr (G::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
-    double2* twl = reinterpret_cast<double2*>(smem + LY::twl_off);
-    const GTw tw = gbl(ap->t.tw), twm = gbl(ap->t.twm);
-    auto stage_copy = [&](auto P_, auto I_) {
-      constexpr int P = decltype(P_)::value, I = decltype(I_)::value;
-      constexpr int q0 = PG::q0(P), mask = (1 << (q0 + I)) - 1;
-      for (int i = threadIdx.x; i < TwLds<N>::mixed_n(P); i += kThreads)
-        twl[TwLds<N>::off(P, I, false) + i] = ld_tw(twm, 2 * mask + i);  // entries mask + la, la < 2^q0
-      for (int i = threadIdx.x; i < TwLds<N>::gen_n(P, I); i += kThreads)
-        twl[TwLds<N>::off(P, I, true) + i] = ld_tw(tw, mask + (1 << q0) + i);
-      if (threadIdx.x == 0) twl[TwLds<N>::fw_off(P, I)] = ld_tw(twm, 2 * (G::L - 1 + q0 + I));
-    };
-    static_assert(G::NPASS == 3 && PG::m(1) == 3 && PG::m(2) == 3, "TwLds: the N = 1024 pass structure");
-    using C0 = std::integral_constant<int, 0>;
-    using C1 = std::integral_constant<int, 1>;
-    using C2 = std::integral_constant<int, 2>;
-    stage_copy(C1{}, C0{}); stage_copy(C1{}, C1{}); stage_copy(C1{}, C2{});
-    stage_copy(C2{}, C0{}); stage_copy(C2{}, C1{}); stage_copy(C2{}, C2{});
+    stage_twiddles<N, 1, 0>(reinterpret_cast<double2*>(smem + LY::twl_off), gbl(ap->t.tw), gbl(ap->t.twm));
   }
   if (ap->need_spectrum && ap->need_mfcc) {
     const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
