@@ -105,9 +105,10 @@ struct Geo {
       cmax(cmax(phys<N>(L - 1) + 1, L + 1), cmax(L + 2 * (L >> 5) + 1, 2 * (kMaxMel + 2 + 64) * 4 / 8));
   // Moment sums through an LDS transpose (5 rows of 64 doubles per wave, row stride 72 so
   // the rows read together fall in different banks) rather than 5 DPP wave sums: measured
-  // faster up to N = 1024 (4+ waves per SIMD), slower at 2048 (2 waves).
+  // faster at every N (at 2048 once it ran in the slot buffer: a table of its own cost 3 waves
+  // their LDS).
 #ifndef MGX_MOM_LDS_MAXN
-#define MGX_MOM_LDS_MAXN 1024
+#define MGX_MOM_LDS_MAXN 2048  // (at 2048 through the slot buffer, MOM_SLOT: 1.5 % faster than DPP sums)
 #endif
   static constexpr bool MOM_LDS = N <= MGX_MOM_LDS_MAXN;
   static constexpr int MOM_STRIDE = 72;
