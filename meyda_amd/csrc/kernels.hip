@@ -85,13 +85,14 @@ struct Geo {
   // allows 4 workgroups per CU; 3 waves (<= 168) at N = 2048 (without the frame prefetch:
   // measured 3 % faster than 2 waves with it). Without the bound the allocator drifts past
   // the threshold (129 VGPRs, or 251 + 32 AGPRs) and occupancy drops.
-  // N = 256 fits 6 waves (<= 80 VGPRs; measured 2.5 % faster than 5); at N = 512 a bound
-  // of 5 waves measured slower than 4.
+  // N = 256 fits 6 waves (<= 80 VGPRs; measured 2.5 % faster than 5); at N = 512 a bound of
+  // 5 waves measured slower than 4 until the LDS twiddles took the passes' global loads out
+  // (81 VGPRs then, 3.9 % faster than 4 waves at 98).
 #ifndef MGX_WPE1024
 #define MGX_WPE1024 4
 #endif
 #ifndef MGX_WPE512
-#define MGX_WPE512 4
+#define MGX_WPE512 5
 #endif
 #ifdef MGX_WPE2048
   static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? MGX_WPE512 : N <= 1024 ? MGX_WPE1024 : MGX_WPE2048;
@@ -101,8 +102,15 @@ struct Geo {
   // Slot buffer entries (8 bytes): the padded exchange image, the natural-order half
   // spectrum X[0..L] (complex output), the padded prefix row (pd) and the mel scratch.
   static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  // (at N = 512 also room for the moment transpose, MOM_SLOT: 41 entries more than the FFT
+  // needs, against the 11.5 KB table it replaces; the workgroup keeps 5 per CU with the
+  // LDS twiddles)
+#ifndef MGX_SLOT_MOM512
+#define MGX_SLOT_MOM512 1
+#endif
   static constexpr int SLOT_PHYS =
-      cmax(cmax(phys<N>(L - 1) + 1, L + 1), cmax(L + 2 * (L >> 5) + 1, 2 * (kMaxMel + 2 + 64) * 4 / 8));
+      cmax(cmax(cmax(phys<N>(L - 1) + 1, L + 1), cmax(L + 2 * (L >> 5) + 1, 2 * (kMaxMel + 2 + 64) * 4 / 8)),
+           (N == 512 && MGX_SLOT_MOM512) ? 5 * 72 : 0);
   // Moment sums through an LDS transpose (5 rows of 64 doubles per wave, row stride 72 so
   // the rows read together fall in different banks) rather than 5 DPP wave sums: measured
   // faster at every N (at 2048 once it ran in the slot buffer: a table of its own cost 3 waves
@@ -127,7 +135,11 @@ struct Geo {
 #ifndef MGX_TW_LDS2048
 #define MGX_TW_LDS2048 1
 #endif
-  static constexpr bool TW_LDS = MGX_TW_LDS && ((N == 1024 && MOM_SLOT) || (N == 2048 && MGX_TW_LDS2048));
+#ifndef MGX_TW_LDS512
+#define MGX_TW_LDS512 1
+#endif
+  static constexpr bool TW_LDS = MGX_TW_LDS && ((N == 1024 && MOM_SLOT) || (N == 2048 && MGX_TW_LDS2048) ||
+                                                (N == 512 && MOM_SLOT && MGX_TW_LDS512));
   // Register prefetch of the next frame. A vector-memory wait is in issue order (vmcnt),
   // so a table load a frame waits on (window, twiddles) also waits for a prefetch issued
   // before it: prefetching at the start of the frame made every frame wait for the next
