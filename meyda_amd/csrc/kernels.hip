@@ -275,17 +275,25 @@ __device__ __forceinline__ int pd(int d) { return d + (d >> 4); }
 // per-frame reductions (moment transpose, prefix and rolloff, band sums, mel scan), 16 the
 // frame start (energy/zcr, window, stage 0), 32 the amplitude, 64 the moment partials.
 // Measured (interleaved A/B, all features): 1 alone 0.5-1 % faster than none;
-// 111 (all but the frame start) another 5.0 % at N = 1024, 4.3 % at 2048, 7.4 % at 512;
-// adding 16 cost N = 512 its fifth wave per SIMD (+7 %).
+// 111 (all but the frame start, level 2) another 5.0 % at N = 1024, 4.3 % at 2048, 7.4 % at 512;
+// then levels: the exchanges and phase 2 at 3, the frame start at 1 (above the FFT's register
+// passes at 0), 127: another 1.4 % at 1024, 2.5 % at 2048, 2.1 % at 512.
 #ifndef MGX_PRIOSET
-#define MGX_PRIOSET 111
+#define MGX_PRIOSET 127
 #endif
 #ifndef MGX_PRIO_P2
-#define MGX_PRIO_P2 2
+#define MGX_PRIO_P2 3
+#endif
+#ifndef MGX_PRIO_XCHG
+#define MGX_PRIO_XCHG 3
+#endif
+#ifndef MGX_PRIO_START
+#define MGX_PRIO_START 1
 #endif
 template <int REGION>
 __device__ __forceinline__ void prio_hi() {
-  if constexpr ((MGX_PRIOSET & REGION) != 0) __builtin_amdgcn_s_setprio(REGION == 4 ? MGX_PRIO_P2 : 2);
+  if constexpr ((MGX_PRIOSET & REGION) != 0)
+    __builtin_amdgcn_s_setprio(REGION == 4 ? MGX_PRIO_P2 : REGION == 1 ? MGX_PRIO_XCHG : REGION == 16 ? MGX_PRIO_START : 2);
 }
 template <int REGION>
 __device__ __forceinline__ void prio_lo() {
