@@ -290,10 +290,28 @@ __device__ __forceinline__ int pd(int d) { return d + (d >> 4); }
 #ifndef MGX_PRIO_START
 #define MGX_PRIO_START 1
 #endif
+#ifndef MGX_PRIO_AMPROW
+#define MGX_PRIO_AMPROW 2
+#endif
+#ifndef MGX_PRIO_RED
+#define MGX_PRIO_RED 2
+#endif
+#ifndef MGX_PRIO_AMP
+#define MGX_PRIO_AMP 2
+#endif
+#ifndef MGX_PRIO_MOM
+#define MGX_PRIO_MOM 2
+#endif
 template <int REGION>
 __device__ __forceinline__ void prio_hi() {
   if constexpr ((MGX_PRIOSET & REGION) != 0)
-    __builtin_amdgcn_s_setprio(REGION == 4 ? MGX_PRIO_P2 : REGION == 1 ? MGX_PRIO_XCHG : REGION == 16 ? MGX_PRIO_START : 2);
+    __builtin_amdgcn_s_setprio(REGION == 4    ? MGX_PRIO_P2
+                               : REGION == 1  ? MGX_PRIO_XCHG
+                               : REGION == 16 ? MGX_PRIO_START
+                               : REGION == 2  ? MGX_PRIO_AMPROW
+                               : REGION == 8  ? MGX_PRIO_RED
+                               : REGION == 32 ? MGX_PRIO_AMP
+                                              : MGX_PRIO_MOM);
 }
 template <int REGION>
 __device__ __forceinline__ void prio_lo() {
