@@ -879,9 +879,13 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
   float2* mud = buf;  // (U, D) of segments 0..nf+1, then the 64 head partials (kMelHead)
   wave_sync();  // band-sum reads of the prefix buffer are done
   float2* mine = mud + lane;  // segment slot `lane` (and lane + 64), head slot kMelHead + lane
-  if (lane < nf + 2) mine[0] = make_float2(0.0f, 0.0f);
-  if (lane + 64 < nf + 2) mine[64] = make_float2(0.0f, 0.0f);
-  wave_sync();
+  // Every segment with a bin is stored by the scan below; only an empty one (b_m = b_{m+1},
+  // 40 bands at N = 512 for example) needs its slot zeroed first (plan flag, one LDS round trip)
+  if (ap->mel_zero) {
+    if (lane < nf + 2) mine[0] = make_float2(0.0f, 0.0f);
+    if (lane + 64 < nf + 2) mine[64] = make_float2(0.0f, 0.0f);
+    wave_sync();
+  }
   f32x2 acc = {0.0f, 0.0f};
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) {

@@ -48,6 +48,7 @@ struct KernelArgs {
   int need_prefix;       // rolloff or loudness: the prefix row (rolloff count, bark band sums)
   int dct_sequential;    // MGX_FLAG_DCT_SEQUENTIAL: the DCT as VALU FMAs in the reference's order
   int mfcc_reference;    // MGX_FLAG_MFCC_REFERENCE: mel sums, log and DCT in the reference's order (SUB kernel)
+  int mel_zero;          // some mel segment [b_m, b_{m+1}) is empty: the scan's slots are zeroed first
 };
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.

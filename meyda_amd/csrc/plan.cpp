@@ -321,6 +321,7 @@ struct mgx_plan {
   mgx::DevTables t{};
   double freq_sum = 0, pow_freq_sum = 0, nyq = 0, sharp_tail = 0;
   int grid_cap = 1;
+  int mel_zero = 1;  // some mel segment is empty (kernels.hip mel_energies)
   // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
   float* s_frames[2] = {nullptr, nullptr};
   unsigned char* s_out[2] = {nullptr, nullptr};
@@ -441,6 +442,9 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
 
   auto* p = new mgx_plan();
   p->d = *d;
+  p->mel_zero = 0;
+  for (int m = 0; m <= nf; ++m)
+    if (bins[m] >= bins[m + 1]) p->mel_zero = 1;
   p->n = n;
   p->L = L;
   // spectralSlope.js:9-16 input-independent sums, in the reference's order
@@ -535,6 +539,7 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.scalar_f64 = (int)p->d.scalar_f64;
   a.dct_sequential = (p->d.flags & MGX_FLAG_DCT_SEQUENTIAL) ? 1 : 0;
   a.mfcc_reference = (p->d.flags & MGX_FLAG_MFCC_REFERENCE) ? 1 : 0;
+  a.mel_zero = p->mel_zero;
   bool spec = o->loudness_specific || o->mfcc || o->amplitude_spectrum || o->power_spectrum || o->complex_real;
   for (int i = MGX_SPECTRAL_CENTROID; i < MGX_NUM_SCALARS; ++i) spec = spec || o->scalars[i];
   a.need_spectrum = spec;
