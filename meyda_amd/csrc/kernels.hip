@@ -671,6 +671,11 @@ __device__ __forceinline__ double wave_inclusive_scan(double v) {
   return v;
 }
 
+// MGX_AMP_MINMAX: the amplitude's per-slot range tests as one unsigned min/max per lane.
+#ifndef MGX_AMP_MINMAX
+#define MGX_AMP_MINMAX 1
+#endif
+
 // Amplitude of one slot: src/meyda.js:104-114, sqrt(re^2 + im^2) in double, stored to float32.
 template <bool FAITH>
 __device__ __forceinline__ float slot_amp(float re, float im) {
@@ -1165,6 +1170,22 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
     float ar[R];
     if constexpr (FAITH) {
+#if MGX_AMP_MINMAX
+      // The range test of every slot as one unsigned min and max of the float bits: each a is
+      // >= +0 or NaN, so unsigned order is float order with NaN above +inf (caught by the max).
+      uint32_t amin = 0xFFFFFFFFu, amax = 0u;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        bool okr;
+        ar[r] = slot_amp_rsq(v[r].x, v[r].y, okr);
+        uint32_t b = __builtin_bit_cast(uint32_t, ar[r]);
+        // (the packed DC/Nyquist slot is replaced below: its range does not matter)
+        if (PG::rpart(G::NPASS - 1, r) == 0) b = dc_lane ? 0x3F800000u : b;
+        amin = min(amin, b);
+        amax = max(amax, b);
+      }
+      const bool ok = amin >= __builtin_bit_cast(uint32_t, 0x1p-40f) && amax <= __builtin_bit_cast(uint32_t, 0x1p60f);
+#else
       bool ok = true;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -1174,6 +1195,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
         if (PG::rpart(G::NPASS - 1, r) == 0) okr = okr || dc_lane;
         ok = ok && okr;
       }
+#endif
       if (__ballot(!ok)) {  // a zero, tiny, huge or non-finite |X|^2 somewhere in the frame
 #pragma unroll
         for (int r = 0; r < R; ++r) ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);
@@ -1649,16 +1671,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
           // total in double (perceptualSpread's (total - max) cancels); max exact in float32;
           // the sharpness weighted sum in float32 (a plain sum of positive terms).
           double tot = sp;
-          float mx = sp, sh = (bnd >= 1 && bnd <= 15) ? (float)bnd * sp : 0.0f;
-          tot += dpp_d<0xB1>(tot); mx = fmaxf(mx, dpp_f<0xB1>(mx)); sh += dpp_f<0xB1>(sh);
-          tot += dpp_d<0x4E>(tot); mx = fmaxf(mx, dpp_f<0x4E>(mx)); sh += dpp_f<0x4E>(sh);
-          tot += dpp_d<0x141>(tot); mx = fmaxf(mx, dpp_f<0x141>(mx)); sh += dpp_f<0x141>(sh);
-          tot += dpp_d<0x140>(tot); mx = fmaxf(mx, dpp_f<0x140>(mx)); sh += dpp_f<0x140>(sh);
+          // (the max on the float bits: every value is >= +0 or NaN, so unsigned order is float
+          // order, and a NaN makes the total NaN either way; one DPP-fused max per step)
+          uint32_t mx = __builtin_bit_cast(uint32_t, sp);
+          float sh = (bnd >= 1 && bnd <= 15) ? (float)bnd * sp : 0.0f;
+          tot += dpp_d<0xB1>(tot); mx = max(mx, (uint32_t)dpp_i<0xB1>((int)mx)); sh += dpp_f<0xB1>(sh);
+          tot += dpp_d<0x4E>(tot); mx = max(mx, (uint32_t)dpp_i<0x4E>((int)mx)); sh += dpp_f<0x4E>(sh);
+          tot += dpp_d<0x141>(tot); mx = max(mx, (uint32_t)dpp_i<0x141>((int)mx)); sh += dpp_f<0x141>(sh);
+          tot += dpp_d<0x140>(tot); mx = max(mx, (uint32_t)dpp_i<0x140>((int)mx)); sh += dpp_f<0x140>(sh);
           // rows 2r and 2r+1 hold one frame: row_bcast:15 adds row 2r's total into row 2r+1
-          tot += dpp_d<0x142, 0xA>(tot); mx = fmaxf(mx, dpp_f<0x142, 0xA>(mx)); sh += dpp_f<0x142, 0xA>(sh);
+          tot += dpp_d<0x142, 0xA>(tot); mx = max(mx, (uint32_t)dpp_i<0x142, 0xA>((int)mx)); sh += dpp_f<0x142, 0xA>(sh);
           if (bnd == 31 && f < q->num_frames) {
             const double rt = rcp_d(tot);  // one reciprocal for both quotients
-            const double ps = (tot - (double)mx) * rt;
+            const double ps = (tot - (double)__builtin_bit_cast(float, mx)) * rt;
             const double sv[3] = {tot, ps * ps, ((double)sh + q->sharp_tail_sum) * (0.11 * rt)};
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
