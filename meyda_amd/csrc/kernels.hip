@@ -800,7 +800,8 @@ struct Lds {
   static constexpr size_t slot_off = 0;
   static constexpr size_t slot_bytes = (size_t)4 * G::SLOT_PHYS * 8;
   static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2 + 64) * 4, "mel scratch must fit");
-  // Per wave, the 5 x 64 table of moment partials (transposed reduction, N <= 512).
+  // Per wave, the 5 x 64 table of moment partials (transposed reduction) when it is not in
+  // the slot buffer (MOM_SLOT: only N = 256 keeps a table of its own).
   static constexpr size_t mom_off = slot_off + slot_bytes;
   static constexpr size_t mom_bytes = (G::MOM_LDS && !G::MOM_SLOT) ? (size_t)4 * 5 * G::MOM_STRIDE * 8 : 0;
   static_assert(!G::MOM_SLOT || (size_t)G::SLOT_PHYS >= (size_t)5 * G::MOM_STRIDE, "moment table must fit the slot buffer");
@@ -1029,10 +1030,10 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
   };
   if (!ap->need_spectrum) prefetch_next();  // time-only features: no table loads follow
-  // The window's table loads are issued before the energy / zcr reductions, so their latency
-  // hides behind them rather than at the window step after the reductions' branches (1 %
-  // faster at N = 512, equal at 1024 and 2048; a lane-major table read as 16-byte loads was
-  // 2-5 % slower at 512 and 2048).
+  // The window: held in registers for the launch at N = 1024 (Geo::WIN_REG); otherwise its
+  // table loads are issued before the energy / zcr reductions, so their latency hides behind
+  // them rather than at the window step after the reductions' branches (1 % faster at
+  // N = 512; a lane-major table read as 16-byte loads was 2-5 % slower at 512 and 2048).
   float wv[CH];
   if (G::WIN_REG) {
 #pragma unroll
@@ -1313,11 +1314,11 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   wave_sync();  // every lane has read the amplitude row: the buffer takes the prefix sums next
   FrameRec& rec = recs[fb];
   // Moments S1..S4 (bin-offset polynomial shift of the local partials) and sum log2 a:
-  // five sums over the lanes. Up to N = 1024 they go through one LDS transpose: lane l
-  // writes column l of a 5 x 64 table; after the prefix scan, lanes 0..39 each add 8
-  // entries (stride 8) of one row and 3 DPP steps finish the row in 8-lane groups; the
-  // table is read back at the end of the frame (after the mel sums). At N = 2048 (2 waves
-  // per SIMD) five DPP wave sums measured faster.
+  // five sums over the lanes, through one LDS transpose: lane l writes column l of a 5 x 64
+  // table, lanes 0..39 each add 8 entries (stride 8) of one row and 3 DPP steps finish the row
+  // in 8-lane groups. With MOM_SLOT (every N but 256) the table is the wave's slot buffer and is
+  // reduced right away, before the prefix row takes the buffer; otherwise it has its own LDS
+  // and is read back at the end of the frame (after the mel sums).
   constexpr bool kMomLds = G::MOM_LDS;
   constexpr int MS = G::MOM_STRIDE;
   // P_p = sum_j (b + j)^p a_j = sum_m C(p, m) b^(p-m) T_m by a Taylor shift (c_i += b c_{i-1},
