@@ -182,9 +182,10 @@ def pmc_live(n, F, precision):
               "mfma": ("all", "SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES "
                               "GRBM_GUI_ACTIVE")}
     got = {}
+    reps = 3
     for key, (fset, ctrs) in passes.items():
         d = os.path.join(tmp, key)
-        env = dict(os.environ, PROBE_SET=fset, PROBE_N=str(n), PROBE_PREC=precision, PROBE_REPS="3", TMPDIR="/tmp")
+        env = dict(os.environ, PROBE_SET=fset, PROBE_N=str(n), PROBE_PREC=precision, PROBE_REPS=str(reps), TMPDIR="/tmp")
         cmd = ["timeout", "-s", "KILL", "90", prof, "--pmc", *ctrs.split(), "--kernel-trace", "--output-format", "csv",
                "-d", d, "-o", "run", "--", sys.executable, probe]
         r = subprocess.run(cmd, env=env, cwd="/tmp", capture_output=True, text=True)
@@ -195,7 +196,8 @@ def pmc_live(n, F, precision):
             for row in csv.DictReader(open(f)):
                 if "extract_kernel" in row.get("Kernel_Name", ""):
                     vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-        got[key] = {k: float(np.mean(v)) for k, v in vals.items()}
+        # per step: a large batch runs as several launches (mgx_extract_device's parts)
+        got[key] = {k: float(np.sum(v)) / reps for k, v in vals.items()}
     shutil.rmtree(tmp, ignore_errors=True)
     frames_bytes = F * n * 4
     cal = frames_bytes / (got["fetch_t"]["FETCH_SIZE"] * 1024)  # true bytes per counted byte (KB counters)

@@ -275,9 +275,10 @@ int mgx_group_info(const mgx_group* group, uint32_t* nranks, uint32_t* first_loc
  * entries, the same on every rank; shard r holds global frames [sum counts[<r],
  * + counts[r])). root_out: device pointers on the root device sized for sum(counts)
  * frames (read on the root only; may be NULL elsewhere); every field in `mask` must be
- * non-NULL there. num_chunks: pipeline depth (0 = automatic). streams[i] (or NULL):
- * the work is ordered after what is enqueued on local rank i's stream, and that stream
- * waits for its completion (gather included). Asynchronous. */
+ * non-NULL there. num_chunks: pipeline depth (0 = automatic). streams: NULL for the
+ * group's own streams, else streams[i] is local rank i's stream (a NULL entry is that
+ * device's default stream): the work is ordered after what is enqueued on it, and it
+ * waits for the work's completion (gather included). Asynchronous. */
 int mgx_group_extract_device(mgx_group* group, const float* const* frames, const uint64_t* counts,
                              const mgx_outputs* root_out, uint32_t mask, uint32_t num_chunks,
                              void* const* streams);

@@ -160,6 +160,7 @@ struct Member {
   mgx_plan* plan = nullptr;
   ncclComm_t comm = nullptr;
   hipStream_t s_comp = nullptr, s_comm = nullptr;
+  hipStream_t s_alt = nullptr;  // the odd chunks' extraction (see mgx_group_extract_device)
   hipEvent_t ev_start = nullptr, ev_comp_done = nullptr, ev_comm_done = nullptr;
   hipEvent_t ev_comp[2] = {nullptr, nullptr}, ev_sent[2] = {nullptr, nullptr};
   unsigned char* xfer = nullptr;  // non-root: 2 packed chunk buffers; root: 2 staging slots per peer
@@ -178,6 +179,7 @@ int member_init(Member& m, const mgx_plan_desc& d) {
   HIP_OK(hipSetDevice(m.device), "hipSetDevice");
   HIP_OK(hipStreamCreateWithFlags(&m.s_comp, hipStreamNonBlocking), "hipStreamCreate");
   HIP_OK(hipStreamCreateWithFlags(&m.s_comm, hipStreamNonBlocking), "hipStreamCreate");
+  HIP_OK(hipStreamCreateWithFlags(&m.s_alt, hipStreamNonBlocking), "hipStreamCreate");
   for (hipEvent_t* e : {&m.ev_start, &m.ev_comp_done, &m.ev_comm_done, &m.ev_comp[0], &m.ev_comp[1], &m.ev_sent[0],
                         &m.ev_sent[1]})
     HIP_OK(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
@@ -188,6 +190,7 @@ void member_free(Member& m) {
   (void)hipSetDevice(m.device);
   if (m.s_comp) (void)hipStreamSynchronize(m.s_comp);  // in-flight kernels read the plan's tables
   if (m.s_comm) (void)hipStreamSynchronize(m.s_comm);
+  if (m.s_alt) (void)hipStreamSynchronize(m.s_alt);
   if (m.plan) mgx_plan_destroy(m.plan);
   m.plan = nullptr;
   if (m.comm) {
@@ -198,6 +201,7 @@ void member_free(Member& m) {
     if (e) (void)hipEventDestroy(e);
   if (m.s_comp) (void)hipStreamDestroy(m.s_comp);
   if (m.s_comm) (void)hipStreamDestroy(m.s_comm);
+  if (m.s_alt) (void)hipStreamDestroy(m.s_alt);
   if (m.xfer) (void)hipFree(m.xfer);
   if (m.h_frames) (void)hipFree(m.h_frames);
   if (m.h_out) (void)hipFree(m.h_out);
@@ -362,8 +366,8 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
   // pipeline depth: about 32 Ki frames per chunk, at most 8 chunks. Each peer's
   // records cross one xGMI link to the root (200 B per frame: ~52 MB per 262,144-frame shard,
   // of the order of the shard's extraction time), so what is not overlapped is about one
-  // chunk's transfer after the last extraction: 8 chunks halve that tail against 4 for ~1 % of
-  // kernel-boundary cost per extra chunk (one-rank group).
+  // chunk's transfer after the last extraction: 8 chunks halve that tail against 4, and the
+  // chunks' kernel boundaries cost nothing on two alternating streams.
   // (a one-rank group has nothing to overlap: one chunk)
   if (nch == 0) nch = R == 1 ? 1 : (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, (most + 32767) / 32768));
   uint64_t cmax = 0;
@@ -383,14 +387,23 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
   // Extraction runs on the caller's stream (or the member's own): no cross-stream wait on
   // the compute path. Transfers and the root's scatters run on the communication stream,
   // ordered after what the caller enqueued before (the scatters write the root's outputs).
+  // A NULL entry of a given array is that device's default stream, as for mgx_extract_device
+  // (it is the stream a caller's earlier work is on; the members' own streams are not ordered
+  // with it, since they are created non-blocking).
+  // Consecutive chunks alternate between that stream and the member's second compute stream:
+  // the chunks are independent, so chunk c+1's workgroups take the slots chunk c's free while
+  // it drains instead of starting after its last workgroup. 8 chunks of 262,144 x 1024 on one
+  // stream took 9 % longer than one launch; alternating, 1 % less. Chunk c and
+  // c+2 share a transfer slot and a stream, so the slot's reuse stays ordered on that stream.
   std::vector<hipStream_t> cs(g->m.size());
   for (size_t i = 0; i < g->m.size(); ++i) {
     Member& m = g->m[i];
-    cs[i] = streams && streams[i] ? static_cast<hipStream_t>(streams[i]) : m.s_comp;
-    if (R == 1) continue;
+    cs[i] = streams ? static_cast<hipStream_t>(streams[i]) : m.s_comp;
+    if (R == 1 && nch == 1) continue;
     HIP_OK(hipSetDevice(m.device), "hipSetDevice");
     HIP_OK(hipEventRecord(m.ev_start, cs[i]), "hipEventRecord");
-    HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_start, 0), "hipStreamWaitEvent");
+    if (nch > 1) HIP_OK(hipStreamWaitEvent(m.s_alt, m.ev_start, 0), "hipStreamWaitEvent");
+    if (R > 1) HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_start, 0), "hipStreamWaitEvent");
   }
   Rccl* rc_ = R > 1 ? rccl() : nullptr;
   if (R > 1 && !rc_) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
@@ -403,20 +416,21 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
       chunk_of(counts[m.rank], nch, c, &c0, &cn);
       HIP_OK(hipSetDevice(m.device), "hipSetDevice");
       const float* src = frames[i] + c0 * N;
+      const hipStream_t st = sl ? m.s_alt : cs[i];
       if (m.rank == 0) {
         if (cn) {
           const mgx_outputs o = offset_outputs(d, *root_out, mask, start[0] + c0);
-          int rc = mgx_extract_device(m.plan, src, cn, &o, cs[i]);
+          int rc = mgx_extract_device(m.plan, src, cn, &o, st);
           if (rc) return rc;
         }
       } else {
-        if (c >= 2) HIP_OK(hipStreamWaitEvent(cs[i], m.ev_sent[sl], 0), "hipStreamWaitEvent");
+        if (c >= 2) HIP_OK(hipStreamWaitEvent(st, m.ev_sent[sl], 0), "hipStreamWaitEvent");
         if (cn) {
           const mgx_outputs o = packed_outputs(d, m.xfer + sl * slot, mask, cn);
-          int rc = mgx_extract_device(m.plan, src, cn, &o, cs[i]);
+          int rc = mgx_extract_device(m.plan, src, cn, &o, st);
           if (rc) return rc;
         }
-        HIP_OK(hipEventRecord(m.ev_comp[sl], cs[i]), "hipEventRecord");
+        HIP_OK(hipEventRecord(m.ev_comp[sl], st), "hipEventRecord");
         HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_comp[sl], 0), "hipStreamWaitEvent");
       }
     }
@@ -466,12 +480,19 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
       }
     }
   }
-  // the callers' streams (or the members' own) wait for the gather
-  for (size_t i = 0; i < g->m.size() && R > 1; ++i) {
+  // the callers' streams (or the members' own) wait for the odd chunks and the gather
+  for (size_t i = 0; i < g->m.size(); ++i) {
     Member& m = g->m[i];
+    if (R == 1 && nch == 1) break;
     HIP_OK(hipSetDevice(m.device), "hipSetDevice");
-    HIP_OK(hipEventRecord(m.ev_comm_done, m.s_comm), "hipEventRecord");
-    HIP_OK(hipStreamWaitEvent(cs[i], m.ev_comm_done, 0), "hipStreamWaitEvent");
+    if (nch > 1) {
+      HIP_OK(hipEventRecord(m.ev_comp_done, m.s_alt), "hipEventRecord");
+      HIP_OK(hipStreamWaitEvent(cs[i], m.ev_comp_done, 0), "hipStreamWaitEvent");
+    }
+    if (R > 1) {
+      HIP_OK(hipEventRecord(m.ev_comm_done, m.s_comm), "hipEventRecord");
+      HIP_OK(hipStreamWaitEvent(cs[i], m.ev_comm_done, 0), "hipStreamWaitEvent");
+    }
   }
   return MGX_OK;
 }

@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --kernel-trace CSV: per kernel name, count / mean / min / max of
 the dispatch durations, over all dispatches and over the LAST k (the timed steps of a
-bench run, after its clock-settle and warmup launches).
-usage: prof_summary.py KERNEL_TRACE.csv [k] [name-substring]"""
+bench run, after its clock-settle and warmup launches). With parts > 1 (a step of the
+bench is that many launches: mgx_extract_device's parts on two streams), the step spans of
+the matching kernel too: first start to last end of each group of `parts` dispatches, over
+the last k steps -- the figure the bench's per-step HIP events measure.
+usage: prof_summary.py KERNEL_TRACE.csv [k] [name-substring] [parts]"""
 import csv
 import sys
 from collections import defaultdict
@@ -12,20 +15,27 @@ def main():
     path = sys.argv[1]
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     sub = sys.argv[3] if len(sys.argv) > 3 else ""
+    parts = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     by = defaultdict(list)
     for row in csv.DictReader(open(path)):
         name = row.get("Kernel_Name", "")
         if sub and sub not in name:
             continue
-        t = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6  # ns -> ms
-        by[name].append((int(row["Start_Timestamp"]), t))
+        t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+        by[name].append((t0, t1))
     print("%-70s %6s %10s %10s %10s %10s" % ("kernel", "n", "mean_ms", "min_ms", "max_ms", "lastK_mean"))
-    for name, v in sorted(by.items(), key=lambda kv: -sum(t for _, t in kv[1])):
+    for name, v in sorted(by.items(), key=lambda kv: -sum(b - a for a, b in kv[1])):
         v.sort()
-        ts = [t for _, t in v]
-        last = ts[-k:]
+        ts = [(b - a) * 1e-6 for a, b in v]  # ns -> ms
+        kk = k * parts
+        last = ts[-kk:]
         print("%-70s %6d %10.4f %10.4f %10.4f %10.4f" % (name[:70], len(ts), sum(ts) / len(ts), min(ts), max(ts),
                                                           sum(last) / len(last)))
+        if parts > 1 and len(v) >= kk and "extract_kernel" in name:
+            tail = v[-kk:]
+            spans = [(max(b for _, b in tail[i:i + parts]) - tail[i][0]) * 1e-6 for i in range(0, kk, parts)]
+            print("  step spans (%d launches per step, last %d steps): mean %.4f ms  min %.4f  max %.4f"
+                  % (parts, k, sum(spans) / len(spans), min(spans), max(spans)))
 
 
 if __name__ == "__main__":
