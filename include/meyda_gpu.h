@@ -265,6 +265,11 @@ int mgx_group_create(const mgx_plan_desc* desc, const int32_t* devices, uint32_t
 int mgx_comm_unique_id(void* id, uint64_t id_bytes);
 int mgx_group_create_rank(const mgx_plan_desc* desc, const void* unique_id, uint32_t nranks, uint32_t rank,
                           mgx_group** out);
+/* Test transport: nranks ranks in this process, all on desc->device, whose chunk transfers
+ * are device copies into the root's staging slots instead of RCCL messages. Everything
+ * else -- shards, chunks, transfer slots, the two compute streams, the root's unpack -- is
+ * the multi-device path's own code, so one GPU can check the gather byte for byte. */
+int mgx_group_create_loopback(const mgx_plan_desc* desc, uint32_t nranks, mgx_group** out);
 int mgx_group_destroy(mgx_group* group);
 /* Ranks of the group, and the ranks this process drives (num_local = 1 per process, or
  * all of them in single-process mode, first_local = their first rank). */

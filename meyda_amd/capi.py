@@ -35,7 +35,7 @@ EXPORTS = ["mgx_plan_desc_init", "mgx_plan_create", "mgx_plan_destroy", "mgx_pla
            "mgx_feature_info", "mgx_device_count", "mgx_abi_version", "mgx_last_error",
            "mgx_wav_parse", "mgx_pcm_decode_device", "mgx_extract_host_pcm",
            "mgx_shard_range", "mgx_packed_layout", "mgx_comm_unique_id", "mgx_group_create",
-           "mgx_group_create_rank", "mgx_group_destroy", "mgx_group_info", "mgx_group_extract_device",
+           "mgx_group_create_rank", "mgx_group_create_loopback", "mgx_group_destroy", "mgx_group_info", "mgx_group_extract_device",
            "mgx_group_extract_host"]
 COMM_ID_BYTES = 128
 FLAG_DCT_SEQUENTIAL = 1  # mgx_plan_desc.flags
@@ -141,6 +141,8 @@ def lib():
                                        ctypes.POINTER(ctypes.c_void_p)]
         L.mgx_group_create_rank.argtypes = [ctypes.POINTER(PlanDesc), ctypes.c_void_p, ctypes.c_uint32,
                                             ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
+        L.mgx_group_create_loopback.argtypes = [ctypes.POINTER(PlanDesc), ctypes.c_uint32,
+                                                ctypes.POINTER(ctypes.c_void_p)]
         L.mgx_group_destroy.argtypes = [ctypes.c_void_p]
         L.mgx_group_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
                                      ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
@@ -372,11 +374,15 @@ class Group:
 
     Group(devices=[0, 1, ...], **plan_kw)                 one process, several devices
     Group(rank=r, nranks=n, unique_id=b, device=d, ...)   one process per device (torchrun)
+    Group(loopback=n, device=d, ...)                      test transport: n ranks on one device
     """
 
-    def __init__(self, buffer_size=512, devices=None, rank=None, nranks=None, unique_id=None, **kw):
+    def __init__(self, buffer_size=512, devices=None, rank=None, nranks=None, unique_id=None, loopback=None, **kw):
         h = ctypes.c_void_p()
-        if devices is not None:
+        if loopback is not None:
+            self.desc = make_desc(buffer_size=buffer_size, **kw)
+            check(lib().mgx_group_create_loopback(ctypes.byref(self.desc), loopback, ctypes.byref(h)))
+        elif devices is not None:
             self.desc = make_desc(buffer_size=buffer_size, device=devices[0], **kw)
             arr = (ctypes.c_int32 * len(devices))(*devices)
             check(lib().mgx_group_create(ctypes.byref(self.desc), arr, len(devices), ctypes.byref(h)))

@@ -224,6 +224,7 @@ struct mgx_group {
   mgx_plan_desc d;
   uint32_t nranks = 0;
   bool single_process = true;
+  bool loopback = false;  // mgx_group_create_loopback: one device, transfers as device copies
   std::vector<Member> m;  // local ranks, in rank order
 };
 
@@ -282,6 +283,30 @@ int mgx_group_create(const mgx_plan_desc* desc, const int32_t* devices, uint32_t
       if (e != ncclSuccess) rc = rccl_fail(e, "ncclCommInitAll");
       else for (uint32_t i = 0; i < ndev; ++i) g->m[i].comm = comms[i];
     }
+  }
+  if (rc) {
+    mgx_group_destroy(g);
+    return rc;
+  }
+  *out = g;
+  return MGX_OK;
+}
+
+int mgx_group_create_loopback(const mgx_plan_desc* desc, uint32_t nranks, mgx_group** out) {
+  if (!out) return fail(MGX_E_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  if (!desc || nranks == 0) return fail(MGX_E_INVALID_ARGUMENT, "a descriptor and at least one rank are required");
+  auto* g = new mgx_group();
+  g->d = *desc;
+  g->nranks = nranks;
+  g->single_process = true;
+  g->loopback = true;
+  g->m.resize(nranks);
+  int rc = MGX_OK;
+  for (uint32_t i = 0; i < nranks && !rc; ++i) {
+    g->m[i].rank = i;
+    g->m[i].device = desc->device;
+    rc = member_init(g->m[i], *desc);
   }
   if (rc) {
     mgx_group_destroy(g);
@@ -405,8 +430,8 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
     if (nch > 1) HIP_OK(hipStreamWaitEvent(m.s_alt, m.ev_start, 0), "hipStreamWaitEvent");
     if (R > 1) HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_start, 0), "hipStreamWaitEvent");
   }
-  Rccl* rc_ = R > 1 ? rccl() : nullptr;
-  if (R > 1 && !rc_) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
+  Rccl* rc_ = R > 1 && !g->loopback ? rccl() : nullptr;
+  if (R > 1 && !g->loopback && !rc_) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
   for (uint32_t c = 0; c < nch; ++c) {
     const int sl = (int)(c & 1);
     // extraction of chunk c on every local rank
@@ -435,6 +460,23 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
       }
     }
     if (R == 1) continue;
+    if (g->loopback) {
+      // the test transport: each peer's chunk copied into the root's staging slot on the
+      // root's communication stream, after the peer's extraction of it
+      Member& root = g->m[0];
+      HIP_OK(hipSetDevice(root.device), "hipSetDevice");
+      for (uint32_t p = 1; p < R; ++p) {
+        Member& m = g->m[p];
+        uint64_t c0, cn;
+        chunk_of(counts[p], nch, c, &c0, &cn);
+        HIP_OK(hipStreamWaitEvent(root.s_comm, m.ev_comp[sl], 0), "hipStreamWaitEvent");
+        if (cn)
+          HIP_OK(hipMemcpyAsync(root.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot, m.xfer + sl * slot,
+                                packed_layout(d, mask, cn, nullptr), hipMemcpyDeviceToDevice, root.s_comm),
+                 "hipMemcpyAsync(loopback chunk)");
+        HIP_OK(hipEventRecord(m.ev_sent[sl], root.s_comm), "hipEventRecord");
+      }
+    } else {
     // transfers of chunk c (one group: in single-process mode it spans every device)
     NCCL_OK(rc_->GroupStart(), "ncclGroupStart");
     for (Member& m : g->m) {
@@ -453,10 +495,11 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
       }
     }
     NCCL_OK(rc_->GroupEnd(), "ncclGroupEnd");
+    }
     for (Member& m : g->m) {
       HIP_OK(hipSetDevice(m.device), "hipSetDevice");
       if (m.rank != 0) {
-        HIP_OK(hipEventRecord(m.ev_sent[sl], m.s_comm), "hipEventRecord");
+        if (!g->loopback) HIP_OK(hipEventRecord(m.ev_sent[sl], m.s_comm), "hipEventRecord");
         continue;
       }
       // scatter each peer's chunk into the root's outputs (ordered after its receive)
@@ -489,7 +532,10 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
       HIP_OK(hipEventRecord(m.ev_comp_done, m.s_alt), "hipEventRecord");
       HIP_OK(hipStreamWaitEvent(cs[i], m.ev_comp_done, 0), "hipStreamWaitEvent");
     }
-    if (R > 1) {
+    if (R > 1 && g->loopback && m.rank != 0) {  // its chunks leave on the root's stream
+      for (uint32_t sl = 0; sl < std::min<uint32_t>(nch, 2); ++sl)
+        HIP_OK(hipStreamWaitEvent(cs[i], m.ev_sent[sl], 0), "hipStreamWaitEvent");
+    } else if (R > 1) {
       HIP_OK(hipEventRecord(m.ev_comm_done, m.s_comm), "hipEventRecord");
       HIP_OK(hipStreamWaitEvent(cs[i], m.ev_comm_done, 0), "hipStreamWaitEvent");
     }

@@ -103,3 +103,34 @@ def test_multi_device_gather(capi):
     torch.cuda.synchronize()
     for k in want:
         assert torch.equal(got[k], want[k]), k
+
+
+@pytest.mark.parametrize("ranks,nch", [(2, 1), (3, 8), (4, 3)])
+def test_loopback_group_gather(capi, ranks, nch):
+    """The gather path of a multi-rank group on one device (mgx_group_create_loopback: chunk
+    transfers as device copies): ragged shards, chunks cycling through the two transfer
+    slots and both compute streams, the root's unpack of every output field. Two calls on
+    different frames: the second's record must not hold anything of the first's."""
+    import torch
+    n, F = 1024, 40001
+    g = capi.Group(buffer_size=n, loopback=ranks, scalar_f64=True)
+    assert (g.nranks, g.first_local, g.num_local) == (ranks, 0, ranks)
+    counts = [capi.shard_range(F, ranks, r)[1] for r in range(ranks)]
+    starts = [capi.shard_range(F, ranks, r)[0] for r in range(ranks)]
+    plan = capi.Plan(buffer_size=n, scalar_f64=True)
+    got, o = plan.alloc_outputs(F, FEATS)
+    stream = torch.cuda.current_stream().cuda_stream
+    for seed_shift in (0, 7919):
+        xs = [_frames(capi, c, n, first=s + seed_shift) for s, c in zip(starts, counts)]
+        for v in got.values():
+            v.fill_(float("nan"))
+        g.extract_device([t.data_ptr() for t in xs], counts, o, capi.output_mask(o), num_chunks=nch,
+                         streams=[stream] * ranks)
+        torch.cuda.synchronize()
+        want = plan.extract_torch(_frames(capi, F, n, first=seed_shift), FEATS)
+        torch.cuda.synchronize()
+        for k in want:
+            a = got[k].view(torch.int32) if got[k].dtype == torch.float32 else got[k].view(torch.int64)
+            b = want[k].view(torch.int32) if want[k].dtype == torch.float32 else want[k].view(torch.int64)
+            assert torch.equal(a, b), (k, seed_shift)
+    g.close()
