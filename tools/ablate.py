@@ -41,10 +41,10 @@ PATCHES = {
     "no_window_load": [("    for (int c = 0; c < CH; ++c) wv[c] = w[c * 64 + lane];",
                         "    for (int c = 0; c < CH; ++c) wv[c] = 0.5f + 0.25f * (c & 1);")],
     # (not an ablation: the DPP wave sums instead of the LDS transpose for the moments at N = 1024)
-    "mom_dpp": [("#define MGX_MOM_LDS_MAXN 1024", "#define MGX_MOM_LDS_MAXN 512")],
+    "mom_dpp": [("#define MGX_MOM_LDS_MAXN 2048", "#define MGX_MOM_LDS_MAXN 512")],
     # the amplitude as |re| + |im| (no f64 squares, no rsq/Heron step)
-    "no_amp": [("        ar[r] = slot_amp_rsq(v[r].x, v[r].y, okr);",
-                "        ar[r] = fabsf(v[r].x) + fabsf(v[r].y); okr = true;")],
+    "no_amp": [("        ar[r] = slot_amp_rsq(v[r].x, v[r].y, okr);\n        uint32_t b",
+                "        ar[r] = fabsf(v[r].x) + fabsf(v[r].y); okr = true;\n        uint32_t b")],
     # the prefix row (stores, rolloff ballots) skipped: band sums read stale LDS
     "no_prefix": [("  const bool need_prefix = SUB ? (bool)ap->need_prefix : true;",
                    "  const bool need_prefix = opaque(0);")],
