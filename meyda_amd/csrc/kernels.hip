@@ -732,7 +732,11 @@ struct FrameRec {
   float lm[kMaxMel];  // mel band energies, then their logs (zero-padded to a multiple of 8)
   int zcr;
   int roll_m;
-  double pad;       // 520 bytes: phase 2 reads across frames hit distinct LDS banks (512 would not)
+  // 520 bytes: phase 2 reads across frames hit distinct LDS banks (512 would not). Phase 2's
+  // loudness step leaves the frame's loudness max (float bits) and sharpness sum here, and
+  // the total in band[0] (the band sums are read by then), for the scalar step.
+  uint32_t loud_max;
+  float sharp_sum;
 };
 
 // Math.pow(x, 0.23) rounded to float32 (loudness.js:62), without the f64 exp/log
@@ -1435,6 +1439,17 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
 // reference's sequential order. The product of two floats is exact in double, so an FMA
 // equals the reference's multiply-then-add. lm and the LDS table are zero-padded to a
 // multiple of 8 bands (0 * 0 adds nothing), so groups of 8 loads issue together.
+// v / d for the DCT's 1 / ncoef scale (mfcc.js:91) without the IEEE division sequence:
+// q0 = v r with r the correctly rounded 1/d, e = v - q0 d (exact by FMA), q0 + e r. By
+// Markstein's theorem that is the correctly rounded quotient -- the division's own result --
+// for every finite nonzero v (tests/test_capi_host.py checks it against v / d); a zero,
+// infinite or NaN v keeps q0, which has the quotient's sign and class there.
+__device__ __forceinline__ double div_by(double v, double d, double r) {
+  const double q0 = v * r;
+  const double q = __builtin_fma(__builtin_fma(-q0, d, v), r, q0);
+  return (q0 != 0.0 && __builtin_fabs(q0) < __builtin_huge_val()) ? q : q0;
+}
+
 __device__ __forceinline__ double dct_sum(const float* dct, const float* lm, int c, int nc, int nfilt) {
   double v = 0.0;
   for (int n0 = 0; n0 < nfilt; n0 += 8) {
@@ -1480,10 +1495,12 @@ __device__ __forceinline__ double rcp_d(double x) {
   return __builtin_fabs(e) < 1.0 ? __builtin_fma(r, e, r) : r;
 }
 
-// One of the ten spectral/time scalars of a frame from its phase-1 record, formulas as
-// written in the reference extractors. Branch-free: every lane evaluates the shared terms
-// (moments, spread) and selects its feature's numerator and denominator, so a wave
-// holding ten different features runs one instruction stream.
+// One of the thirteen scalars of a frame from its record (phase 1's sums, phase 2's loudness
+// entries), formulas as written in the reference extractors. Branch-free: every lane
+// evaluates the shared terms (moments, spread) and selects its feature's numerator and
+// denominator, so a wave holding thirteen different features runs one instruction stream
+// (the loudness quotients joined it from a tail of their own: one reciprocal chain per batch
+// instead of three).
 template <int N>
 __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int sc) {
   constexpr int L = N / 2;
@@ -1493,7 +1510,7 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   const double inv = rcp_d(S0);
   const double m1 = rc.S[1] * inv, m2 = rc.S[2] * inv, m3 = rc.S[3] * inv, m4 = rc.S[4] * inv;
   const double sd = sqrt_d(m2 - m1 * m1);  // spectralSpread.js
-  double num, den = 1.0;
+  double num, den = 1.0, k = 1.0;
   switch (sc) {  // selects only (no divergent code: every case is a few operands)
     case MGX_RMS: num = rc.energy * (1.0 / N); break;  // rms.js: sqrt(sum / N), N a power of 2
     case MGX_ENERGY: num = rc.energy; break;           // energy.js
@@ -1513,13 +1530,24 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
       num = 2.0 * m1 * m1 * m1 - 3.0 * m1 * m2 + m3;
       den = sd * sd * sd;
       break;
-    default:                                           // spectralKurtosis.js (6 mu1 mu2 as written)
+    case MGX_SPECTRAL_KURTOSIS:                        // spectralKurtosis.js (6 mu1 mu2 as written)
       num = -3.0 * m1 * m1 * m1 * m1 + 6.0 * m1 * m2 - 4.0 * m1 * m3 + m4;
       den = sd * sd * sd * sd;
       break;
+    // the loudness total (double, loudness.js:67-69) in band[0], from phase 2's loudness step
+    case MGX_LOUDNESS_TOTAL: num = rc.band[0]; break;
+    case MGX_PERCEPTUAL_SPREAD:                        // perceptualSpread.js:7-12, squared below
+      num = rc.band[0] - (double)__builtin_bit_cast(float, rc.loud_max);
+      den = rc.band[0];
+      break;
+    default:                                           // perceptualSharpness.js:7-14 (0.11 / total)
+      num = (double)rc.sharp_sum + q->sharp_tail_sum;
+      den = rc.band[0];
+      k = 0.11;
+      break;
   }
-  const double v = num * rcp_d(den);
-  return sc == MGX_RMS ? sqrt_d(v) : v;
+  const double v = num * (k * rcp_d(den));
+  return sc == MGX_RMS ? sqrt_d(v) : sc == MGX_PERCEPTUAL_SPREAD ? v * v : v;
 }
 
 // Copy of the TwLds image from the plan tables, once per workgroup (before its LDS barrier).
@@ -1682,17 +1710,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
           tot += dpp_d<0x140>(tot); mx = max(mx, (uint32_t)dpp_i<0x140>((int)mx)); sh += dpp_f<0x140>(sh);
           // rows 2r and 2r+1 hold one frame: row_bcast:15 adds row 2r's total into row 2r+1
           tot += dpp_d<0x142, 0xA>(tot); mx = max(mx, (uint32_t)dpp_i<0x142, 0xA>((int)mx)); sh += dpp_f<0x142, 0xA>(sh);
-          if (bnd == 31 && f < q->num_frames) {
-            const double rt = rcp_d(tot);  // one reciprocal for both quotients
-            const double ps = (tot - (double)__builtin_bit_cast(float, mx)) * rt;
-            const double sv[3] = {tot, ps * ps, ((double)sh + q->sharp_tail_sum) * (0.11 * rt)};
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-              void* dst = q->out.scalars[MGX_LOUDNESS_TOTAL + k];
-              if (!dst) continue;
-              if (q->scalar_f64) gbl(static_cast<double*>(dst))[f] = sv[k];
-              else gbl(static_cast<float*>(dst))[f] = (float)sv[k];
-            }
+          // the three quotients are formed in the scalar step below, with the others
+          if (bnd == 31) {
+            recs[fb].band[0] = tot;
+            recs[fb].loud_max = mx;
+            recs[fb].sharp_sum = sh;
           }
         }
       }
@@ -1723,7 +1745,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
           const int c = i / FPW, fb = i % FPW;
           const uint64_t f = f0 + fb;
           const double v = dct_sum(dct_lds, recs[fb].lm, c, nc, nfilt);
-          if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(v / nc);
+          if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)div_by(v, nc, q->rcp_ncoef);
         }
         } else {
         // mfcc.js:85-93 on the FP64 matrix cores, v_mfma_f64_4x4x4_4b_f64: 4 blocks of a
@@ -1747,13 +1769,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
           }
           const int c = mt + 4 * ((l2 >> 2) & 3) + kk;
           const uint64_t f = f0 + fa;
-          if (c < nc && f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)(acc / nc);
+          if (c < nc && f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)div_by(acc, nc, q->rcp_ncoef);
         }
         }
       }
       MGX_MARK(dct_done);
-      // the other scalar features: one lane per (feature, frame)
-      for (int i = l2; i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {
+      // the scalar features: one lane per (feature, frame); the loudness total, perceptual
+      // spread and sharpness from the loudness step's record entries (16 x 4 lanes at most)
+      for (int i = l2; i < (MGX_PERCEPTUAL_SHARPNESS + 1) * FPW; i += 64) {
         const int sc = i / FPW, fb = i % FPW;
         const uint64_t f = f0 + fb;
         void* dst = reinterpret_cast<void* const*>(smem + LY::kc_off)[sc];

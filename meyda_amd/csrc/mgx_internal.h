@@ -38,6 +38,7 @@ struct KernelArgs {
   double pow_freq_sum;   // spectralSlope.js: sum of (i*sr/N)^2
   double nyq_bin;        // spectralRolloff.js:4: sr / (2 (N/2 - 1))
   double sharp_tail_sum; // perceptualSharpness.js:10: sum_{i=15}^{23} 0.066 e^{0.171 (i+1)}
+  double rcp_ncoef;      // 1 / ncoef, correctly rounded: the DCT's scale as Markstein quotients (div_by)
   int nfilt;
   int ncoef;
   int scalar_f64;

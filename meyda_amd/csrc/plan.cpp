@@ -534,6 +534,7 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.pow_freq_sum = p->pow_freq_sum;
   a.nyq_bin = p->nyq;
   a.sharp_tail_sum = p->sharp_tail;
+  a.rcp_ncoef = 1.0 / (double)p->d.num_mfcc_coeffs;
   a.nfilt = (int)p->d.num_mel_bands;
   a.ncoef = (int)p->d.num_mfcc_coeffs;
   a.scalar_f64 = (int)p->d.scalar_f64;

@@ -143,3 +143,56 @@ int main(void) {
     exe = tmp_path / "div"
     subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(src), "-lm"])
     assert subprocess.check_output([str(exe)]).decode().strip() == "0"
+
+
+def test_dct_scale_division_is_correctly_rounded(tmp_path):
+    """kernels.hip div_by: the DCT's v / ncoef (mfcc.js:91) as q0 = v r, fma(fma(-q0, d, v), r, q0)
+    with r = 1/d (Markstein). Equal to the IEEE quotient for every divisor 1..64 on 2^21
+    random doubles per divisor spread over 2^-60..2^60 and both signs, plus the exact
+    multiples; zeros and non-finite v keep q0."""
+    import shutil
+    import subprocess
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    src = tmp_path / "divby.c"
+    src.write_text(r"""
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+static uint64_t s = 0x6D657964u;
+static uint64_t next(void) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static double div_by(double v, double d, double r) {
+  const double q0 = v * r;
+  const double q = fma(fma(-q0, d, v), r, q0);
+  return (q0 != 0.0 && fabs(q0) < HUGE_VAL) ? q : q0;
+}
+static int same(double a, double b) { return memcmp(&a, &b, 8) == 0 || (a != a && b != b); }
+int main(void) {
+  long bad = 0;
+  for (int d = 1; d <= 64; ++d) {
+    volatile double dd = d, r = 1.0 / dd;
+    for (int i = 0; i < (1 << 21); ++i) {
+      const uint64_t u = next();
+      double v = ldexp((double)(u >> 11) * 0x1p-53 + 0.5, (int)(u % 121) - 60);
+      if (u & 1024) v = -v;
+      volatile double vv = v;
+      if (!same(div_by(vv, dd, r), vv / dd)) ++bad;
+      volatile double m = (double)(int64_t)(u >> 40) * dd;  /* exact multiples */
+      if (!same(div_by(m, dd, r), m / dd)) ++bad;
+    }
+    const double sp[] = {0.0, -0.0, HUGE_VAL, -HUGE_VAL, NAN};
+    for (int k = 0; k < 5; ++k) if (!same(div_by(sp[k], dd, r), sp[k] / dd)) ++bad;
+  }
+  printf("%ld\n", bad);
+  return 0;
+}
+""")
+    exe = tmp_path / "divby"
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(src), "-lm"])
+    assert subprocess.check_output([str(exe)], timeout=120).decode().strip() == "0"

@@ -1,3 +1,3 @@
-set -o pipefail
-timeout -k 10 300 python tools/ab_libs.py --rounds 7 base=abl/lib_base.so winreg=abl/lib_winreg.so pf1=abl/lib_pf1.so pf0=abl/lib_pf0.so || exit 1
-echo "== C3 features (SUB kernel)"; timeout -k 10 200 python tools/ab_libs.py --rounds 5 --features spectralCentroid,spectralFlatness,spectralSlope,spectralRolloff,spectralSpread,spectralSkewness,spectralKurtosis,loudness,perceptualSpread,perceptualSharpness base=abl/lib_base.so winreg=abl/lib_winreg.so pf1=abl/lib_pf1.so pf0=abl/lib_pf0.so || exit 1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/trim_tests.log 2>&1 || { tail -30 gpurun_out/trim_tests.log; exit 1; }
+tail -1 gpurun_out/trim_tests.log
+VARIANTS="base=abl/lib_base.so trim=abl/lib_trim.so" bash tools/gpu_ab3.sh
