@@ -1501,7 +1501,7 @@ __device__ __forceinline__ double rcp_d(double x) {
 // denominator, so a wave holding thirteen different features runs one instruction stream
 // (the loudness quotients joined it from a tail of their own: one reciprocal chain per batch
 // instead of three).
-template <int N>
+template <int N, bool SUB>
 __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int sc) {
   constexpr int L = N / 2;
   const double S0 = rc.S[0];
@@ -1509,7 +1509,17 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   // 0, >= 2^-149 or non-finite, so 1/S0 neither overflows nor hides a NaN of the quotient)
   const double inv = rcp_d(S0);
   const double m1 = rc.S[1] * inv, m2 = rc.S[2] * inv, m3 = rc.S[3] * inv, m4 = rc.S[4] * inv;
-  const double sd = sqrt_d(m2 - m1 * m1);  // spectralSpread.js
+  // A feature subset (SUB) forms the square root and the geometric mean only when the request
+  // reads S2..S4 / sum log2 a (a wave-uniform branch: C2's centroid alone skips them)
+  double sd = 0.0, geo = 0.0;
+  if constexpr (SUB) {
+    if (q->need_mom > 1) {
+      sd = sqrt_d(m2 - m1 * m1);
+      geo = exp2_mean(rc.ln2sum * (1.0 / L)) * L;
+    }
+  } else {
+    sd = sqrt_d(m2 - m1 * m1);  // spectralSpread.js
+  }
   double num, den = 1.0, k = 1.0;
   switch (sc) {  // selects only (no divergent code: every case is a few operands)
     case MGX_RMS: num = rc.energy * (1.0 / N); break;  // rms.js: sqrt(sum / N), N a power of 2
@@ -1517,7 +1527,7 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
     case MGX_ZCR: num = (double)rc.zcr; break;         // zcr.js
     case MGX_SPECTRAL_CENTROID: num = m1; break;       // spectralCentroid.js
     case MGX_SPECTRAL_FLATNESS:                        // spectralFlatness.js: geometric / arithmetic mean
-      num = exp2_mean(rc.ln2sum * (1.0 / L)) * L;
+      num = SUB ? geo : exp2_mean(rc.ln2sum * (1.0 / L)) * L;
       den = S0;
       break;
     case MGX_SPECTRAL_SLOPE:                           // spectralSlope.js:9-21
@@ -1781,7 +1791,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         const uint64_t f = f0 + fb;
         void* dst = reinterpret_cast<void* const*>(smem + LY::kc_off)[sc];
         if (f >= q->num_frames || dst == nullptr) continue;
-        const double v = scalar_value<N>(q, recs[fb], sc);
+        const double v = scalar_value<N, SUB>(q, recs[fb], sc);
         if (q->scalar_f64) gbl(static_cast<double*>(dst))[f] = v;
         else gbl(static_cast<float*>(dst))[f] = (float)v;
       }
