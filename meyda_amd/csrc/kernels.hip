@@ -1063,7 +1063,11 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   const float e32 = e2.x + e2.y;
   int z = 0;
   uint64_t pge = 0, plt = 0;
-  if (__ballot(e32 != e32)) {
+  // (a feature subset, SUB, skips the ballots without zcr and the wave sum without rms /
+  // energy; the lane partials e32 stay: the FFT's range test reads them)
+  const bool want_zcr = !SUB || ap->need_zcr, want_energy = !SUB || ap->need_energy;
+  if (!want_zcr) {
+  } else if (__ballot(e32 != e32)) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const uint64_t g = __ballot(x[c] >= 0.0f), l = __ballot(x[c] < 0.0f);
@@ -1084,8 +1088,9 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
   // float32 partial sums are within 1e-6 relative of the double sum; a wave whose
   // partials leave [2^-100, 2^100] (silence, denormal or huge input) redoes it in double.
-  double e;
-  if (__ballot(!(e32 >= 0x1p-100f && e32 <= 0x1p100f))) {
+  double e = 0.0;
+  if (!want_energy) {
+  } else if (__ballot(!(e32 >= 0x1p-100f && e32 <= 0x1p100f))) {
     double e64 = 0.0;
 #pragma unroll
     for (int c = 0; c < CH; ++c) e64 = __builtin_fma((double)x[c], (double)x[c], e64);
@@ -1889,9 +1894,9 @@ template <int N>
 hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, hipStream_t stream) {
   if (mode == MGX_MODE_LITERAL) return launch_n<N, true, true>(a, grid, stream);
   if (precision == MGX_PRECISION_FAST) return launch_n<N, false, false>(a, grid, stream);
-  // a spectral feature subset that skips the moment / prefix work takes the SUB kernel
+  // a spectral feature subset that skips the moment / prefix / time-domain work takes the SUB kernel
   // (and so does MGX_FLAG_MFCC_REFERENCE: the all-feature kernel keeps its schedule)
-  if (a.need_spectrum && (!(a.need_mom == 2 && a.need_prefix) || a.mfcc_reference))
+  if (a.need_spectrum && (!(a.need_mom == 2 && a.need_prefix && a.need_energy && a.need_zcr) || a.mfcc_reference))
     return launch_n<N, true, false, true>(a, grid, stream);
   return launch_n<N, true, false>(a, grid, stream);
 }

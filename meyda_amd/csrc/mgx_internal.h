@@ -47,6 +47,8 @@ struct KernelArgs {
   int need_mfcc;
   int need_mom;          // 2: flatness / spread / skewness / kurtosis (S1..S4, sum log2 a); 1: centroid / slope (S1); 0
   int need_prefix;       // rolloff or loudness: the prefix row (rolloff count, bark band sums)
+  int need_energy;       // rms or energy: the wave sum of the squares (SUB kernel)
+  int need_zcr;          // zcr: the sign-change ballots (SUB kernel)
   int dct_sequential;    // MGX_FLAG_DCT_SEQUENTIAL: the DCT as VALU FMAs in the reference's order
   int mfcc_reference;    // MGX_FLAG_MFCC_REFERENCE: mel sums, log and DCT in the reference's order (SUB kernel)
   int mel_zero;          // some mel segment [b_m, b_{m+1}) is empty: the scan's slots are zeroed first

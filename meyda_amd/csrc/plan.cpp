@@ -552,6 +552,8 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
                 o->scalars[MGX_SPECTRAL_SKEWNESS] || o->scalars[MGX_SPECTRAL_KURTOSIS]) ? 2
                : (o->scalars[MGX_SPECTRAL_CENTROID] || o->scalars[MGX_SPECTRAL_SLOPE]) ? 1 : 0;
   a.need_prefix = a.need_loudness || o->scalars[MGX_SPECTRAL_ROLLOFF];
+  a.need_energy = o->scalars[MGX_RMS] || o->scalars[MGX_ENERGY];
+  a.need_zcr = o->scalars[MGX_ZCR] != nullptr;
   const uint64_t fb = (uint64_t)mgx::frames_per_batch(p->n);
   const uint64_t nb = (nframes + fb - 1) / fb;
   const int grid = (int)std::min<uint64_t>(nb, (uint64_t)p->grid_cap);
