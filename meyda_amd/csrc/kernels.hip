@@ -1280,6 +1280,9 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // every feature is requested and the branches compile away (the all-feature kernel keeps
   // its schedule: run-time branches there cost 0.7 %).
   const int mom_level = SUB ? ap->need_mom : 2;
+  // light: a subset reading neither the moments nor the prefix row (mfcc alone, spectra):
+  // no amplitude total, no scan; the non-finite test from the amplitudes' float bits
+  const bool light = SUB && mom_level == 0 && !ap->need_prefix;
   const bool need_mom = mom_level > 0, need_hi = mom_level > 1;
   double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
   float l2f = 0.0f;
@@ -1314,9 +1317,18 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       T0 += ad;
       if (jj > 0) T1 = __builtin_fma((double)jj, ad, T1);
     }
-  } else {
+  } else if (!light) {
 #pragma unroll
     for (int jj = 0; jj < R; ++jj) T0 += (double)av[jj];
+  }
+  // (every amplitude is >= +0 or NaN: unsigned order of the bits is float order, NaN and
+  // +inf on top; one max per slot, as the amplitude's range test)
+  bool light_nonfinite = false;
+  if (light) {
+    uint32_t am = 0u;
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) am = max(am, __builtin_bit_cast(uint32_t, av[jj]));
+    light_nonfinite = __ballot(am >= 0x7F800000u) != 0;
   }
   MGX_MARK(moments_done);
   prio_hi<8>();
@@ -1353,9 +1365,12 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
   }
   // prefix P(k) = sum_{i<k} a_i: lane-exclusive offset + local prefix
-  const double incl = wave_inclusive_scan(T0);
-  const double excl = dpp_d<0x138>(incl);  // wave_shr:1 (lane 0 reads 0)
-  const double total = readlane_d(incl, 63);
+  double excl = 0.0, total = 0.0;
+  if (!light) {
+    const double incl = wave_inclusive_scan(T0);
+    excl = dpp_d<0x138>(incl);  // wave_shr:1 (lane 0 reads 0)
+    total = readlane_d(incl, 63);
+  }
   // the moment transpose's reduction (lanes 0..39: 8 entries of one row, then 3 DPP steps)
   auto mom_reduce = [&]() {
     const int row = lane < 40 ? lane >> 3 : 0;
@@ -1423,7 +1438,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // mel bands over all bins in reference order (mfcc.js:53-62).
   // (total = sum of the amplitudes in double: non-finite iff some amplitude is.)
   MGX_MARK(bands_done);
-  if (!(total < __builtin_huge_val())) {
+  if (light ? light_nonfinite : !(total < __builtin_huge_val())) {
     nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
   } else if (SUB && ap->need_mfcc && ap->mfcc_reference) {  // (the all-feature kernel never has the flag)
     mel_reference_order<N>(ap, av, lane, buf, rec);

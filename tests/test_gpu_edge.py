@@ -95,6 +95,26 @@ def test_nonfinite_and_extreme_frames(capi, oracle_mod, n):
     compare(out, ref, n)
 
 
+@pytest.mark.parametrize("n", [256, 512, 1024, 2048])
+def test_subsets_match_full_request_on_edge_frames(capi, n):
+    """A feature subset runs the SUB kernel, which skips what the request does not read (zcr
+    ballots, the energy sum, moments, the prefix row and, without both, the amplitude total:
+    the non-finite test then comes from the amplitudes' bits). Its outputs must equal the
+    all-feature kernel's bit for bit, on the NaN / Inf / overflow / denormal frames too."""
+    x = np.concatenate([edge_frames(n), np.random.default_rng(n).uniform(-1, 1, (40, n)).astype(np.float32)])
+    plan = capi.Plan(buffer_size=n, scalar_f64=True)
+    full = plan.extract(x, FEATS)
+    for feats in (["mfcc"], ["amplitudeSpectrum", "spectralCentroid"], ["mfcc", "powerSpectrum"],
+                  ["spectralKurtosis", "loudness"], ["zcr", "mfcc"], ["rms", "spectralRolloff"]):
+        out = plan.extract(x, feats)
+        for k, v in out.items():
+            if k not in full:
+                continue
+            a, b = np.asarray(v), np.asarray(full[k])
+            same = (a.view(np.uint8) == b.view(np.uint8)).reshape(a.shape + (-1,)).all(-1) | (np.isnan(a) & np.isnan(b))
+            assert same.all(), (feats, k, np.nonzero(~same)[0][:5])
+
+
 @pytest.mark.parametrize("sr", [8000.0, 22050.0, 48000.0, 96000.0])
 def test_sample_rates(capi, oracle_mod, sr):
     n = 1024
