@@ -8,10 +8,10 @@ mkdir -p $O && cd $R
 timeout -k 10 400 python bench.py > $O/bench.log 2>&1
 rc=$?; tail -1 $O/bench.log; [ $rc -ne 0 ] && exit $rc
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 10 --no-cpu-baseline --no-host-path --no-pmc --no-every-output > $O/prof_bench.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 100 --warmup 20 --no-cpu-baseline --no-host-path --no-pmc --no-every-output > $O/prof_bench.log 2>&1
 rc=$?; tail -1 $O/prof_bench.log; [ $rc -ne 0 ] && exit $rc
 f=$(find $O/prof -name "*kernel_trace.csv" | head -1)
-python3 $R/tools/prof_summary.py $f 20 > $O/prof_summary.txt && cat $O/prof_summary.txt
+python3 $R/tools/prof_summary.py $f 100 > $O/prof_summary.txt && cat $O/prof_summary.txt
 cd $R
 timeout -k 10 300 python tools/configs_bench.py > $O/configs.log 2>&1
 rc=$?; cat $O/configs.log | grep config; [ $rc -ne 0 ] && exit $rc
