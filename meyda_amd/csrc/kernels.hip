@@ -1713,39 +1713,41 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       KArgs* q = args_ptr();
       const int l2 = opaque(lane);
       if (q->need_spectrum && q->need_loudness) {
-        // 32 lanes per frame (24 bands + 8 idle), so a frame's reductions stay in two DPP rows.
-#pragma unroll
-        for (int i0 = 0; i0 < FPW * 32; i0 += 64) {
-          const int i = i0 + l2;
-          const int fb = i >> 5, bnd = i & 31;
-          const uint64_t f = f0 + fb;
-          const bool live = bnd < kBark;
-          const double sum = recs[fb].band[live ? bnd : 0];
-          // loudness.js:62 Math.pow(sum, 0.23), stored to Float32Array
-          float sp = pow023(sum);
-          if (!live) sp = 0.0f;
-          if (live && f < q->num_frames && q->out.loudness_specific) gbl(q->out.loudness_specific)[f * kBark + bnd] = sp;
-          // loudness.js:67-69 total; perceptualSpread.js:7-12 max; perceptualSharpness.js:7-14
-          // (off-by-one spec[i+1] for i < 15, then the constant 0.066 e^{0.171 (i+1)} tail).
-          // total in double (perceptualSpread's (total - max) cancels); max exact in float32;
-          // the sharpness weighted sum in float32 (a plain sum of positive terms).
-          double tot = sp;
-          // (the max on the float bits: every value is >= +0 or NaN, so unsigned order is float
-          // order, and a NaN makes the total NaN either way; one DPP-fused max per step)
-          uint32_t mx = __builtin_bit_cast(uint32_t, sp);
-          float sh = (bnd >= 1 && bnd <= 15) ? (float)bnd * sp : 0.0f;
-          tot += dpp_d<0xB1>(tot); mx = max(mx, (uint32_t)dpp_i<0xB1>((int)mx)); sh += dpp_f<0xB1>(sh);
-          tot += dpp_d<0x4E>(tot); mx = max(mx, (uint32_t)dpp_i<0x4E>((int)mx)); sh += dpp_f<0x4E>(sh);
-          tot += dpp_d<0x141>(tot); mx = max(mx, (uint32_t)dpp_i<0x141>((int)mx)); sh += dpp_f<0x141>(sh);
-          tot += dpp_d<0x140>(tot); mx = max(mx, (uint32_t)dpp_i<0x140>((int)mx)); sh += dpp_f<0x140>(sh);
-          // rows 2r and 2r+1 hold one frame: row_bcast:15 adds row 2r's total into row 2r+1
-          tot += dpp_d<0x142, 0xA>(tot); mx = max(mx, (uint32_t)dpp_i<0x142, 0xA>((int)mx)); sh += dpp_f<0x142, 0xA>(sh);
-          // the three quotients are formed in the scalar step below, with the others
-          if (bnd == 31) {
-            recs[fb].band[0] = tot;
-            recs[fb].loud_max = mx;
-            recs[fb].sharp_sum = sh;
-          }
+        // 16 lanes per frame, two bands each (24 bands in lanes 0..11 of the row, 12..15 idle):
+        // the four frames of the batch in one pass, a frame's reductions in one DPP row. The
+        // lane's pair sum is the reduction tree's first level and the four row steps the rest,
+        // so every partial sum is the one the 32-lane layout formed (same results).
+        static_assert(FPW * 16 == 64, "one DPP row per frame of the batch");
+        const int fb = l2 >> 4, pr = l2 & 15;
+        const uint64_t f = f0 + fb;
+        const bool live = pr < kBark / 2;
+        const int b0 = live ? 2 * pr : 0;
+        const double sum0 = recs[fb].band[b0], sum1 = recs[fb].band[b0 + 1];
+        // loudness.js:62 Math.pow(sum, 0.23), stored to Float32Array
+        float sp0 = pow023(sum0), sp1 = pow023(sum1);
+        if (!live) sp0 = sp1 = 0.0f;
+        if (live && f < q->num_frames && q->out.loudness_specific)
+          *reinterpret_cast<__attribute__((address_space(1))) f32x2*>(gbl(q->out.loudness_specific) + f * kBark + b0) =
+              f32x2{sp0, sp1};
+        // loudness.js:67-69 total; perceptualSpread.js:7-12 max; perceptualSharpness.js:7-14
+        // (off-by-one spec[i+1] for i < 15, then the constant 0.066 e^{0.171 (i+1)} tail).
+        // total in double (perceptualSpread's (total - max) cancels); max exact in float32;
+        // the sharpness weighted sum in float32 (a plain sum of positive terms).
+        double tot = (double)sp0 + (double)sp1;
+        // (the max on the float bits: every value is >= +0 or NaN, so unsigned order is float
+        // order, and a NaN makes the total NaN either way; one DPP-fused max per step)
+        uint32_t mx = max(__builtin_bit_cast(uint32_t, sp0), __builtin_bit_cast(uint32_t, sp1));
+        float sh = ((b0 >= 1 && b0 <= 15) ? (float)b0 * sp0 : 0.0f) + ((b0 + 1 <= 15) ? (float)(b0 + 1) * sp1 : 0.0f);
+        tot += dpp_d<0xB1>(tot); mx = max(mx, (uint32_t)dpp_i<0xB1>((int)mx)); sh += dpp_f<0xB1>(sh);
+        tot += dpp_d<0x4E>(tot); mx = max(mx, (uint32_t)dpp_i<0x4E>((int)mx)); sh += dpp_f<0x4E>(sh);
+        tot += dpp_d<0x141>(tot); mx = max(mx, (uint32_t)dpp_i<0x141>((int)mx)); sh += dpp_f<0x141>(sh);
+        tot += dpp_d<0x140>(tot); mx = max(mx, (uint32_t)dpp_i<0x140>((int)mx)); sh += dpp_f<0x140>(sh);
+        // (every lane of the row holds the frame's sums; the three quotients are formed in the
+        // scalar step below, with the others)
+        if (pr == 15) {
+          recs[fb].band[0] = tot;
+          recs[fb].loud_max = mx;
+          recs[fb].sharp_sum = sh;
         }
       }
       MGX_MARK(loud2_done);

@@ -3,7 +3,7 @@
 §5.4 rule 24): each build (abl/libabl_*.so or any libmeyda_gpu.so copy) is loaded with its
 own ctypes handle; per round, every variant times 20 launches of the all-feature batch
 (262,144 x N=1024 unless --n/--frames); prints the median and min per variant.
-usage: ab_libs.py [--n N] [--frames F] [--rounds R] NAME=PATH[:flags] ...   (PATH 'base' = the tree's library)"""
+usage: ab_libs.py [--n N] [--frames F] [--rounds R] [--compare] NAME=PATH[:flags] ...   (PATH 'base' = the tree's library)"""
 import argparse
 import ctypes
 import os
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--frames", type=int, default=262144)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--features", default="all")
+    ap.add_argument("--compare", action="store_true", help="also check every variant's outputs against the first's, bit for bit")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     n, F = a.n, a.frames
@@ -70,6 +71,20 @@ def main():
             e1.record(s)
             torch.cuda.synchronize()
             res[name].append(e0.elapsed_time(e1) / 20)
+    if a.compare:
+        first = None
+        for name, L, h in vs:
+            got, og = plan0.alloc_outputs(F, feats)
+            for t in got.values():
+                t.fill_(float("nan"))
+            L.mgx_extract_device(h, ctypes.c_void_p(x.data_ptr()), F, ctypes.byref(og), ctypes.c_void_p(s.cuda_stream))
+            torch.cuda.synchronize()
+            bits = {k: t.view(torch.int32 if t.element_size() == 4 else torch.int64) for k, t in got.items()}
+            if first is None:
+                first = bits
+                continue
+            diff = [k for k in bits if not torch.equal(bits[k], first[k])]
+            print("%-14s outputs %s" % (name, "identical to %s" % vs[0][0] if not diff else "DIFFER in %s" % diff))
     base = np.median(res[vs[0][0]])
     for name, _, _ in vs:
         m = np.median(res[name])
