@@ -165,6 +165,14 @@ struct Geo {
 #define MGX_WIN_REG 1
 #endif
   static constexpr bool WIN_REG = MGX_WIN_REG && N == 1024;
+  // BLIM_REG: each band lane's two prefix-row offsets (bark limits, loudness.js:25-45) held in
+  // one packed register for the launch instead of read from LDS per frame (N <= 512: -0.5 %;
+  // at 1024 the register spills two others, +1.3 %; at 2048 a value kept live across the
+  // frame loop spills)
+#ifndef MGX_BLIM_REG
+#define MGX_BLIM_REG 1
+#endif
+  static constexpr bool BLIM_REG = MGX_BLIM_REG && N <= 512;
   static constexpr bool PREFETCH = PF != 0;
 #ifdef MGX_LPREMAT
   static constexpr bool LPREMAT = MGX_LPREMAT;
@@ -1018,7 +1026,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
                                              int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
                                              const int* klim, float (&xn)[Geo<N>::PREFETCH ? Geo<N>::CH : 1],
-                                             GF next, const double2* twl, const float (&wreg)[Geo<N>::CH]) {
+                                             GF next, const double2* twl, const float (&wreg)[Geo<N>::CH],
+                                             uint32_t blim) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
@@ -1424,8 +1433,12 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
   MGX_MARK(prefetch_issued);
   if (need_prefix && lane < kBark) {
-    const int lb = opaque(lane);  // (an address kept live across the frame loop spills at N = 2048)
-    rec.band[lb] = pbuf[pd(klim[lb + 1])] - pbuf[pd(klim[lb])];  // limits staged in LDS
+    if constexpr (G::BLIM_REG) {
+      rec.band[lane] = pbuf[blim >> 16] - pbuf[blim & 0xFFFFu];
+    } else {
+      const int lb = opaque(lane);  // (an address kept live across the frame loop spills at N = 2048)
+      rec.band[lb] = pbuf[pd(klim[lb + 1])] - pbuf[pd(klim[lb])];  // limits staged in LDS
+    }
   }
   if (lane == 0) {
     rec.S[0] = total;
@@ -1670,6 +1683,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     for (int c = 0; c < CH; ++c) xv[c] = ld_frame(xin + c * 64);
   };
 
+  // the band lane's prefix-row offsets pd(lim[b]) | pd(lim[b + 1]) << 16 (G::BLIM_REG)
+  uint32_t blim = 0;
+  if constexpr (G::BLIM_REG) {
+    const int* kl = reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8);
+    const int lb = lane < kBark ? lane : 0;
+    blim = (uint32_t)pd(kl[lb]) | ((uint32_t)pd(kl[lb + 1]) << 16);
+  }
   float wreg[CH];
   if constexpr (G::WIN_REG) {
     const GF w = gbl(ap->t.window);
@@ -1700,7 +1720,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       }
       frame_phase1<N, FAITH, LITERAL, SUB>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
                                       reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
-                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg);
+                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim);
     }
     wave_sync();
 

@@ -1,3 +1,4 @@
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/trim_tests.log 2>&1 || { tail -30 gpurun_out/trim_tests.log; exit 1; }
-tail -1 gpurun_out/trim_tests.log
-VARIANTS="base=abl/lib_base.so trim=abl/lib_trim.so" bash tools/gpu_ab3.sh
+for cfg in "1024 262144" "2048 131072" "512 262144"; do
+  n=${cfg% *}; f=${cfg#* }
+  echo "== N=$n"; timeout -k 10 200 python tools/ab_libs.py --rounds 7 --compare --n $n --frames $f head=abl/lib_head.so blim=abl/lib_blim.so || exit 1
+done
