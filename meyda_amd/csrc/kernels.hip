@@ -1775,10 +1775,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         // mfcc.js:64 Math.log of the band energies, stored to Float32Array
         const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
         const bool ref_log = SUB && q->mfcc_reference;  // the double Math.log, then float32
-        for (int i = l2; i < FPW * nfp; i += 64) {
-          const int band = i / FPW, fb = i % FPW;
-          recs[fb].lm[band] = band < nfilt ? (ref_log ? (float)log((double)recs[fb].lm[band]) : ln_f32(recs[fb].lm[band]))
-                                           : 0.0f;  // padding for dct_sum
+        // two bands per lane (a pair of adjacent floats: one LDS read and write each): the
+        // batch's 4 frames x 32 bands in one pass
+        auto ln1 = [&](float v, int band) {
+          return band < nfilt ? (ref_log ? (float)log((double)v) : ln_f32(v)) : 0.0f;  // padding for dct_sum
+        };
+        for (int i = l2; i < FPW * (nfp / 2); i += 64) {
+          const int fb = i % FPW, band = 2 * (i / FPW);
+          f32x2* pp = reinterpret_cast<f32x2*>(&recs[fb].lm[band]);
+          const f32x2 v = *pp;
+          *pp = f32x2{ln1(v.x, band), ln1(v.y, band + 1)};
         }
       }
     }
