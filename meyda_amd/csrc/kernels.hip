@@ -1021,7 +1021,7 @@ __device__ __forceinline__ void mel_reference_order(KArgs* ap, const float (&av)
 }
 
 // One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
-template <int N, bool FAITH, bool LITERAL, bool SUB>
+template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
                                              int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
@@ -1288,10 +1288,10 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // the non-finite test). SUB: a feature subset, the flags are read at run time; otherwise
   // every feature is requested and the branches compile away (the all-feature kernel keeps
   // its schedule: run-time branches there cost 0.7 %).
-  const int mom_level = SUB ? ap->need_mom : 2;
+  const int mom_level = LIGHT ? 0 : SUB ? ap->need_mom : 2;
   // light: a subset reading neither the moments nor the prefix row (mfcc alone, spectra):
   // no amplitude total, no scan; the non-finite test from the amplitudes' float bits
-  const bool light = SUB && mom_level == 0 && !ap->need_prefix;
+  const bool light = LIGHT || (SUB && mom_level == 0 && !ap->need_prefix);
   const bool need_mom = mom_level > 0, need_hi = mom_level > 1;
   double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
   float l2f = 0.0f;
@@ -1398,7 +1398,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // spectralRolloff.js:6-15: the largest m with P(m) <= 0.99 total (P(0) = 0).
   const double thr = 0.99 * total;
   int cnt = 0;
-  const bool need_prefix = SUB ? (bool)ap->need_prefix : true;
+  const bool need_prefix = LIGHT ? false : SUB ? (bool)ap->need_prefix : true;
   if (need_prefix) {
     double pk = excl;  // P(R lane + jj), accumulated again rather than kept (registers)
 #pragma unroll
@@ -1612,7 +1612,7 @@ __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
   }
 }
 
-template <int N, bool FAITH, bool LITERAL, bool SUB>
+template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
@@ -1718,7 +1718,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       } else {
         load(x, b, j);
       }
-      frame_phase1<N, FAITH, LITERAL, SUB>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
+      frame_phase1<N, FAITH, LITERAL, SUB, LIGHT>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
                                       reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
                                       reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim);
     }
@@ -1732,7 +1732,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     {
       KArgs* q = args_ptr();
       const int l2 = opaque(lane);
-      if (q->need_spectrum && q->need_loudness) {
+      if (!LIGHT && q->need_spectrum && q->need_loudness) {
         // 16 lanes per frame, two bands each (24 bands in lanes 0..11 of the row, 12..15 idle):
         // the four frames of the batch in one pass, a frame's reductions in one DPP row. The
         // lane's pair sum is the reduction tree's first level and the four row steps the rest,
@@ -1907,17 +1907,17 @@ __global__ void unpack_kernel(UnpackArgs a) {
     dst[i] = src[i];
 }
 
-template <int N, bool FAITH, bool LITERAL, bool SUB = false>
+template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false>
 hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
   const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
-  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB>), dim3(grid), dim3(kThreads), lds, stream, a);
+  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT>), dim3(grid), dim3(kThreads), lds, stream, a);
   return hipGetLastError();
 }
 
-template <int N, bool FAITH, bool LITERAL, bool SUB = false>
+template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false>
 int occupancy_n(size_t lds) {
   int blocks = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL, SUB>, kThreads, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL, SUB, LIGHT>, kThreads, lds) !=
       hipSuccess)
     return 0;
   return blocks;
@@ -1928,9 +1928,10 @@ int occupancy_prec(int precision, int mode, int ncoef, int nfilt) {
   const size_t lds = Lds<N>::bytes(ncoef, nfilt);
   if (mode == MGX_MODE_LITERAL) return occupancy_n<N, true, true>(lds);
   if (precision == MGX_PRECISION_FAST) return occupancy_n<N, false, false>(lds);
-  // the grid serves both faithful kernels (all features / a subset)
-  const int a = occupancy_n<N, true, false>(lds), b = occupancy_n<N, true, false, true>(lds);
-  return a < b ? a : b;
+  // the grid serves the three faithful kernels (all features / a subset / a light subset)
+  const int a = occupancy_n<N, true, false>(lds), b = occupancy_n<N, true, false, true>(lds),
+            c = occupancy_n<N, true, false, true, true>(lds);
+  return a < b ? (a < c ? a : c) : (b < c ? b : c);
 }
 
 template <int N>
@@ -1939,6 +1940,10 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
   if (precision == MGX_PRECISION_FAST) return launch_n<N, false, false>(a, grid, stream);
   // a spectral feature subset that skips the moment / prefix / time-domain work takes the SUB kernel
   // (and so does MGX_FLAG_MFCC_REFERENCE: the all-feature kernel keeps its schedule)
+  // (LIGHT: a subset reading neither the moments nor the prefix row, e.g. mfcc or the spectra
+  // alone, compiled without that code: no runtime branches to keep its registers live)
+  if (a.need_spectrum && a.need_mom == 0 && !a.need_prefix && !a.mfcc_reference)
+    return launch_n<N, true, false, true, true>(a, grid, stream);
   if (a.need_spectrum && (!(a.need_mom == 2 && a.need_prefix && a.need_energy && a.need_zcr) || a.mfcc_reference))
     return launch_n<N, true, false, true>(a, grid, stream);
   return launch_n<N, true, false>(a, grid, stream);
