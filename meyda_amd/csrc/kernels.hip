@@ -1021,7 +1021,7 @@ __device__ __forceinline__ void mel_reference_order(KArgs* ap, const float (&av)
 }
 
 // One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
-template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT>
+template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
                                              int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
@@ -1074,7 +1074,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   uint64_t pge = 0, plt = 0;
   // (a feature subset, SUB, skips the ballots without zcr and the wave sum without rms /
   // energy; the lane partials e32 stay: the FFT's range test reads them)
-  const bool want_zcr = !SUB || ap->need_zcr, want_energy = !SUB || ap->need_energy;
+  // (NOTIME: the all-feature kernel's schedule without rms / energy / zcr, compiled out)
+  const bool want_zcr = SUB ? (bool)ap->need_zcr : !NOTIME, want_energy = SUB ? (bool)ap->need_energy : !NOTIME;
   if (!want_zcr) {
   } else if (__ballot(e32 != e32)) {
 #pragma unroll
@@ -1612,7 +1613,7 @@ __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
   }
 }
 
-template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT>
+template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
@@ -1718,7 +1719,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       } else {
         load(x, b, j);
       }
-      frame_phase1<N, FAITH, LITERAL, SUB, LIGHT>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
+      frame_phase1<N, FAITH, LITERAL, SUB, LIGHT, NOTIME>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
                                       reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
                                       reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim);
     }
@@ -1907,17 +1908,17 @@ __global__ void unpack_kernel(UnpackArgs a) {
     dst[i] = src[i];
 }
 
-template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false>
+template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false>
 hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
   const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
-  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT>), dim3(grid), dim3(kThreads), lds, stream, a);
+  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME>), dim3(grid), dim3(kThreads), lds, stream, a);
   return hipGetLastError();
 }
 
-template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false>
+template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false>
 int occupancy_n(size_t lds) {
   int blocks = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL, SUB, LIGHT>, kThreads, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME>, kThreads, lds) !=
       hipSuccess)
     return 0;
   return blocks;
@@ -1928,10 +1929,13 @@ int occupancy_prec(int precision, int mode, int ncoef, int nfilt) {
   const size_t lds = Lds<N>::bytes(ncoef, nfilt);
   if (mode == MGX_MODE_LITERAL) return occupancy_n<N, true, true>(lds);
   if (precision == MGX_PRECISION_FAST) return occupancy_n<N, false, false>(lds);
-  // the grid serves the three faithful kernels (all features / a subset / a light subset)
-  const int a = occupancy_n<N, true, false>(lds), b = occupancy_n<N, true, false, true>(lds),
-            c = occupancy_n<N, true, false, true, true>(lds);
-  return a < b ? (a < c ? a : c) : (b < c ? b : c);
+  // the grid serves the four faithful kernels (all features / without the time-domain ones /
+  // a subset / a light subset)
+  int m = occupancy_n<N, true, false>(lds);
+  for (int o : {occupancy_n<N, true, false, false, false, true>(lds), occupancy_n<N, true, false, true>(lds),
+                occupancy_n<N, true, false, true, true>(lds)})
+    m = o < m ? o : m;
+  return m;
 }
 
 template <int N>
@@ -1944,6 +1948,10 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
   // alone, compiled without that code: no runtime branches to keep its registers live)
   if (a.need_spectrum && a.need_mom == 0 && !a.need_prefix && !a.mfcc_reference)
     return launch_n<N, true, false, true, true>(a, grid, stream);
+  // (NOTIME: every spectral sum but no rms / energy / zcr, e.g. C3: the all-feature schedule
+  // with the time-domain reductions compiled out)
+  if (a.need_spectrum && a.need_mom == 2 && a.need_prefix && !a.need_energy && !a.need_zcr && !a.mfcc_reference)
+    return launch_n<N, true, false, false, false, true>(a, grid, stream);
   if (a.need_spectrum && (!(a.need_mom == 2 && a.need_prefix && a.need_energy && a.need_zcr) || a.mfcc_reference))
     return launch_n<N, true, false, true>(a, grid, stream);
   return launch_n<N, true, false>(a, grid, stream);
