@@ -1819,11 +1819,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         const int kk = l2 >> 4, fa = l2 & 3, nsteps = (nfilt + 3) >> 2;
         const float* lmrow = recs[fa].lm;
         for (int mt = 0; mt < nc; mt += 16) {
-          const int ca = mt + (l2 & 15);
+          // (a tile row past the last coefficient reads the last row again instead of a
+          // guarded zero: a row of A only feeds its own coefficient's outputs, never stored)
+          const int ca = min(mt + (l2 & 15), nc - 1);
           double acc = 0.0;
           for (int st = 0; st < nsteps; ++st) {
             const int n = 4 * st + kk;  // < nfilt rounded up to 8: the tables are zero-padded
-            const float av = ca < nc ? dct_lds[ca + n * nc] : 0.0f;
+            const float av = dct_lds[ca + n * nc];
             acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)av, (double)lmrow[n], acc, 0, 0, 0);
           }
           const int c = mt + 4 * ((l2 >> 2) & 3) + kk;

@@ -3,14 +3,16 @@
 listing built with -DMGX_MARKS (tools/isa.sh OUT.s -DMGX_MARKS): the instructions between
 consecutive `;mgxmark` comments, by class (f64 arithmetic, f32<->f64 conversions, other
 VALU, LDS, vector memory, scalar).
-usage: isa_phases.py FILE.s [N] [SUB]"""
+usage: isa_phases.py FILE.s [N] [SUB[,LIGHT[,NOTIME]]]"""
 import re
 import sys
 from collections import Counter, OrderedDict
 
 
 def kernel_lines(path, n, sub):
-    name = "_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb1ELb0ELb%dEEEvNS_10KernelArgsE" % (n, sub)
+    # extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME>; sub = SUB or "sub,light,notime"
+    flags = [int(v) for v in str(sub).split(",")] + [0, 0]
+    name = "_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb1ELb0ELb%dELb%dELb%dEEEvNS_10KernelArgsE" % (n, *flags[:3])
     lines = open(path).read().split("\n")
     start = [i for i, l in enumerate(lines) if l.startswith(name + ":")][0]
     out = []
@@ -40,7 +42,7 @@ def cls(op):
 def main():
     path = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
-    sub = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    sub = sys.argv[3] if len(sys.argv) > 3 else "0"
     seg = "prologue"
     counts = OrderedDict()
     order = []
