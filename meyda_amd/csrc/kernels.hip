@@ -1530,11 +1530,9 @@ __device__ __forceinline__ double rcp_d(double x) {
 }
 
 // One of the thirteen scalars of a frame from its record (phase 1's sums, phase 2's loudness
-// entries), formulas as written in the reference extractors. Branch-free: every lane
-// evaluates the shared terms (moments, spread) and selects its feature's numerator and
-// denominator, so a wave holding thirteen different features runs one instruction stream
-// (the loudness quotients joined it from a tail of their own: one reciprocal chain per batch
-// instead of three).
+// entries), formulas as written in the reference extractors. Every lane evaluates the shared
+// terms (moments, spread) and takes its feature's numerator and denominator (the loudness
+// quotients joined from a tail of their own: one reciprocal chain per batch instead of three).
 template <int N, bool SUB>
 __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int sc) {
   constexpr int L = N / 2;
@@ -1555,7 +1553,9 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
     sd = sqrt_d(m2 - m1 * m1);  // spectralSpread.js
   }
   double num, den = 1.0, k = 1.0;
-  switch (sc) {  // selects only (no divergent code: every case is a few operands)
+  // (at thirteen cases the compiler lowers the switch to a branch tree the wave runs case by
+  // case; one lane per frame in straight-line code instead measured 0.4-0.6 % slower)
+  switch (sc) {
     case MGX_RMS: num = rc.energy * (1.0 / N); break;  // rms.js: sqrt(sum / N), N a power of 2
     case MGX_ENERGY: num = rc.energy; break;           // energy.js
     case MGX_ZCR: num = (double)rc.zcr; break;         // zcr.js
