@@ -9,7 +9,9 @@ of 1024 float32 samples per GPU (BASELINE config C3/C4 size), computing every
 per-frame feature: rms, energy, zcr, spectralCentroid/Flatness/Slope/Rolloff/
 Spread/Skewness/Kurtosis, loudness (24 specific + total), perceptualSpread,
 perceptualSharpness, mfcc (13 coefficients of the reference's 26 mel bands).
-Inputs are generated in HBM before the timed region.
+Inputs are generated in HBM before the timed region. Consecutive steps alternate
+between two streams and two output sets, as a caller streaming batches runs them: one
+launch's drain (its last waves leaving the SIMDs) overlaps the next launch's start.
 
 Multi-GPU (torchrun, one process per GPU): each rank extracts its own 262,144-frame
 shard of one global stream (weak scaling) through the library's multi-device group
@@ -129,18 +131,33 @@ def capi_seed():
 
 def settle(step, ms, dist=None):
     """Untimed steps for `ms` of wall time (clock ramp-up), before the warmup steps."""
-    stream = torch.cuda.current_stream()
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     t0 = time.perf_counter()
     go = True
     while go:
-        for _ in range(8):
-            step(stream.cuda_stream)
+        pipelined(step, streams, 0, 8)
         torch.cuda.synchronize()
         go = (time.perf_counter() - t0) * 1e3 < ms
         if dist:  # every rank runs the same number of (collective) steps
             t = torch.tensor([1 if go else 0], dtype=torch.int32)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             go = bool(t.item())
+
+
+def pipelined(step, streams, first, count):
+    """Steps first..first+count-1, consecutive steps alternating between the two streams and
+    the two output sets (step(stream, k), k = i & 1): a stream of batches the way a streaming
+    caller runs it, so step i+1's workgroups start on the CUs step i's last waves leave while it
+    drains (one launch ends with ~45 us of SIMDs running out of waves). Forks
+    from and joins back into streams[0]."""
+    e = torch.cuda.Event()
+    e.record(streams[0])
+    streams[1].wait_event(e)
+    for i in range(first, first + count):
+        step(streams[i & 1].cuda_stream, i & 1)
+    e = torch.cuda.Event()
+    e.record(streams[1])
+    streams[0].wait_event(e)
 
 
 def host_path(plan, frames, reps=3):
@@ -219,28 +236,38 @@ def pmc_live(n, F, precision):
 
 def run_mode(step, steps, warmup, dist):
     """W untimed steps, then exactly `steps` timed ones bracketed by a barrier and a device
-    synchronisation on both sides; HIP events on the launch stream around each step."""
-    stream = torch.cuda.current_stream()
-    for _ in range(warmup):
-        step(stream.cuda_stream)
+    synchronisation on both sides, pipelined over two streams (pipelined()); HIP events on the
+    launch stream around the whole timed region give the launch period (no events between the
+    steps: an event pair per step cost 1-2 % of the step time, tools/step_overlap.py). Then an
+    untimed single-stream pass with an event pair around each launch: the launch duration on
+    its own, which is what rocprofv3 reports per dispatch."""
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    pipelined(step, streams, 0, warmup)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for i in range(steps):
-        ev[i][0].record(stream)
-        step(stream.cuda_stream)
-        ev[i][1].record(stream)
+    e0.record(streams[0])
+    pipelined(step, streams, 0, steps)
+    e1.record(streams[0])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    per_step = [a.elapsed_time(b) for a, b in ev]
-    kernel_ms = float(np.mean(per_step))
-    stats = {"mean_ms": kernel_ms, "median_ms": float(np.median(per_step)), "min_ms": float(np.min(per_step)),
-             "max_ms": float(np.max(per_step))}
+    period = e0.elapsed_time(e1) / steps
+    # the launch on its own (serialised on one stream), untimed by the step clock
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+    for a, b in ev:
+        a.record(streams[0])
+        step(streams[0].cuda_stream, 0)
+        b.record(streams[0])
+    torch.cuda.synchronize()
+    iso = [a.elapsed_time(b) for a, b in ev]
+    stats = {"period_ms": period, "launch_alone_mean_ms": float(np.mean(iso)),
+             "launch_alone_median_ms": float(np.median(iso)), "launch_alone_min_ms": float(np.min(iso)),
+             "launch_alone_max_ms": float(np.max(iso))}
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -248,9 +275,9 @@ def run_mode(step, steps, warmup, dist):
         # per-GPU step times reported separately (HIP events on each rank's stream)
         allr = [None] * dist.get_world_size()
         dist.all_gather_object(allr, stats)
-        stats = {"rank0": stats, "per_rank_mean_ms": [r["mean_ms"] for r in allr],
-                 "per_rank_median_ms": [r["median_ms"] for r in allr]}
-    return elapsed, kernel_ms, stats
+        stats = {"rank0": stats, "per_rank_period_ms": [r["period_ms"] for r in allr],
+                 "per_rank_launch_alone_ms": [r["launch_alone_mean_ms"] for r in allr]}
+    return elapsed, period, stats
 
 
 def main():
@@ -277,17 +304,18 @@ def main():
         group = capi.Group(buffer_size=n, rank=rank, nranks=world, unique_id=uid[0], precision=args.precision,
                            device=dev)
         # rank 0 holds the whole job's feature record; the other ranks only their transfer buffers
-        outs, o = plan.alloc_outputs(F * world if rank == 0 else 1, FEATURES)
-        mask = capi.output_mask(o)
-        root = o if rank == 0 else None
+        # (two output sets: consecutive steps are in flight together, pipelined())
+        sets = [plan.alloc_outputs(F * world if rank == 0 else 1, FEATURES) for _ in range(2)]
+        mask = capi.output_mask(sets[0][1])
 
-        def step(s):
-            group.extract_device([frames.data_ptr()], [F] * world, root, mask, args.chunks, [s])
+        def step(s, k):
+            group.extract_device([frames.data_ptr()], [F] * world, sets[k][1] if rank == 0 else None, mask,
+                                 args.chunks, [s])
     else:
-        outs, o = plan.alloc_outputs(F, FEATURES)
+        sets = [plan.alloc_outputs(F, FEATURES) for _ in range(2)]
 
-        def step(s):
-            plan.extract_device(frames.data_ptr(), F, o, s)
+        def step(s, k):
+            plan.extract_device(frames.data_ptr(), F, sets[k][1], s)
     torch.cuda.synchronize()
     settle(step, args.settle_ms, dist)
     elapsed, kernel_ms, step_stats = run_mode(step, args.steps, args.warmup, dist)
@@ -295,8 +323,8 @@ def main():
     if args.also_fast and args.precision != "fast" and world == 1:
         plan_f = capi.Plan(buffer_size=n, precision="fast", device=dev)
 
-        def step_f(s):
-            plan_f.extract_device(frames.data_ptr(), F, o, s)
+        def step_f(s, k):
+            plan_f.extract_device(frames.data_ptr(), F, sets[k][1], s)
         settle(step_f, args.settle_ms)
         el_f, km_f, _ = run_mode(step_f, args.steps, args.warmup, dist)
         fast = {"value": world * F * args.steps / el_f, "kernel_ms": km_f,
@@ -307,19 +335,20 @@ def main():
         # amplitude, power and complex spectra — with the 40-band mel of config C4, same frames
         plan_e = capi.Plan(buffer_size=n, precision=args.precision, num_mel_bands=40, device=dev)
         feats_e = FEATURES + ["amplitudeSpectrum", "powerSpectrum", "complexSpectrum"]
-        outs_e, o_e = plan_e.alloc_outputs(F, feats_e)
+        sets_e = [plan_e.alloc_outputs(F, feats_e) for _ in range(2)]
 
-        def step_e(s):
-            plan_e.extract_device(frames.data_ptr(), F, o_e, s)
+        def step_e(s, k):
+            plan_e.extract_device(frames.data_ptr(), F, sets_e[k][1], s)
         settle(step_e, args.settle_ms)
         el_e, km_e, _ = run_mode(step_e, args.steps, args.warmup, dist)
         bpf_e = 4 * n + 4 * (OUT_FLOATS + 2 * (n // 2) + 2 * n)
         every = {"features": feats_e, "mel_bands": 40, "value": F * args.steps / el_e, "unit": "frames/s",
                  "kernel_ms": km_e, "bytes_per_frame": bpf_e,
                  "roofline_frac": F * bpf_e / (km_e * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        del outs_e, o_e
+        del sets_e
     if rank == 0:
         bytes_per_frame = 4 * n + 4 * OUT_FLOATS
+        alone_ms = (step_stats["rank0"] if dist else step_stats)["launch_alone_median_ms"]
         achieved = F * bytes_per_frame / (kernel_ms * 1e-3) / 1e9
         traffic, valu, traffic_note = None, None, "not measured (--no-pmc or N > 1)"
         if world == 1 and not args.no_pmc:
@@ -363,6 +392,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                          "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
+                         "kernel_ms_source": "launch period: HIP events around the timed region / steps "
+                                             "(steps pipelined over two streams); a launch on its own: step_event_ms",
+                         "frac_launch_alone": F * bytes_per_frame / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "step_event_ms": step_stats,
                          "bytes_per_frame": bytes_per_frame},
         }

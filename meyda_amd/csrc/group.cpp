@@ -163,6 +163,9 @@ struct Member {
   hipStream_t s_alt = nullptr;  // the odd chunks' extraction (see mgx_group_extract_device)
   hipEvent_t ev_start = nullptr, ev_comp_done = nullptr, ev_comm_done = nullptr;
   hipEvent_t ev_comp[2] = {nullptr, nullptr}, ev_sent[2] = {nullptr, nullptr};
+  // a transfer slot's last send was recorded in ev_sent (by this call or an earlier one: a call
+  // on another stream may start before the previous call's sends are done)
+  bool xfer_sent[2] = {false, false};
   unsigned char* xfer = nullptr;  // non-root: 2 packed chunk buffers; root: 2 staging slots per peer
   uint64_t xfer_bytes = 0;
   float* h_frames = nullptr;       // mgx_group_extract_host: this device's shard
@@ -449,7 +452,7 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
           if (rc) return rc;
         }
       } else {
-        if (c >= 2) HIP_OK(hipStreamWaitEvent(st, m.ev_sent[sl], 0), "hipStreamWaitEvent");
+        if (c >= 2 || m.xfer_sent[sl]) HIP_OK(hipStreamWaitEvent(st, m.ev_sent[sl], 0), "hipStreamWaitEvent");
         if (cn) {
           const mgx_outputs o = packed_outputs(d, m.xfer + sl * slot, mask, cn);
           int rc = mgx_extract_device(m.plan, src, cn, &o, st);
@@ -475,6 +478,7 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
                                 packed_layout(d, mask, cn, nullptr), hipMemcpyDeviceToDevice, root.s_comm),
                  "hipMemcpyAsync(loopback chunk)");
         HIP_OK(hipEventRecord(m.ev_sent[sl], root.s_comm), "hipEventRecord");
+        m.xfer_sent[sl] = true;
       }
     } else {
     // transfers of chunk c (one group: in single-process mode it spans every device)
@@ -499,7 +503,10 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
     for (Member& m : g->m) {
       HIP_OK(hipSetDevice(m.device), "hipSetDevice");
       if (m.rank != 0) {
-        if (!g->loopback) HIP_OK(hipEventRecord(m.ev_sent[sl], m.s_comm), "hipEventRecord");
+        if (!g->loopback) {
+          HIP_OK(hipEventRecord(m.ev_sent[sl], m.s_comm), "hipEventRecord");
+          m.xfer_sent[sl] = true;
+        }
         continue;
       }
       // scatter each peer's chunk into the root's outputs (ordered after its receive)

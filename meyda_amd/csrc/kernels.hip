@@ -1296,17 +1296,23 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   const bool need_mom = mom_level > 0, need_hi = mom_level > 1;
   double T0 = 0, T1 = 0, T2 = 0, T3 = 0, T4 = 0;
   float l2f = 0.0f;
+  // (the sums start from bins 0 and 1 instead of from 0.0: every amplitude is >= +0 or NaN,
+  // so 0 + a and fma(1, a, 0) are a itself -- the same sums without the no-op adds)
   if (need_hi) {
+    T0 = (double)av[0];
+    {
+      const double a1 = av[1];
+      T0 += a1;
+      T1 = T2 = T3 = T4 = a1;
+    }
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) {
+    for (int jj = 2; jj < R; ++jj) {
       const double ad = av[jj];
       T0 += ad;
-      if (jj > 0) {
-        T1 = __builtin_fma((double)jj, ad, T1);
-        T2 = __builtin_fma((double)(jj * jj), ad, T2);
-        T3 = __builtin_fma((double)(jj * jj * jj), ad, T3);
-        T4 = __builtin_fma((double)(jj * jj * jj * jj), ad, T4);
-      }
+      T1 = __builtin_fma((double)jj, ad, T1);
+      T2 = __builtin_fma((double)(jj * jj), ad, T2);
+      T3 = __builtin_fma((double)(jj * jj * jj), ad, T3);
+      T4 = __builtin_fma((double)(jj * jj * jj * jj), ad, T4);
     }
     // sum log2 a by pairs, log2(a_j a_{j+1}) with the bare v_log_f32 (== log2f for normal
     // inputs; one hardware log per two bins, and the product's rounding is ~2^-24 relative,
@@ -1321,15 +1327,19 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       for (int jj = 0; jj < R; ++jj) l2f += log2f(av[jj]);
     }
   } else if (need_mom) {
+    T0 = (double)av[0];
+    T1 = av[1];
+    T0 += T1;
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) {
+    for (int jj = 2; jj < R; ++jj) {
       const double ad = av[jj];
       T0 += ad;
-      if (jj > 0) T1 = __builtin_fma((double)jj, ad, T1);
+      T1 = __builtin_fma((double)jj, ad, T1);
     }
   } else if (!light) {
+    T0 = (double)av[0];
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) T0 += (double)av[jj];
+    for (int jj = 1; jj < R; ++jj) T0 += (double)av[jj];
   }
   // (every amplitude is >= +0 or NaN: unsigned order of the bits is float order, NaN and
   // +inf on top; one max per slot, as the amplitude's range test)

@@ -134,3 +134,39 @@ def test_loopback_group_gather(capi, ranks, nch):
             b = want[k].view(torch.int32) if want[k].dtype == torch.float32 else want[k].view(torch.int64)
             assert torch.equal(a, b), (k, seed_shift)
     g.close()
+
+
+@pytest.mark.parametrize("ranks,nch", [(2, 8), (3, 3)])
+def test_loopback_group_calls_overlap_on_two_streams(capi, ranks, nch):
+    """Consecutive group calls on two different streams (as bench.py pipelines its steps): the
+    second call's first chunks reuse the transfer slots of the first call's last ones, so they
+    must wait for those sends; both records must match one plan's extraction byte for byte."""
+    import torch
+    n, F = 1024, 30011
+    g = capi.Group(buffer_size=n, loopback=ranks, scalar_f64=True)
+    counts = [capi.shard_range(F, ranks, r)[1] for r in range(ranks)]
+    starts = [capi.shard_range(F, ranks, r)[0] for r in range(ranks)]
+    plan = capi.Plan(buffer_size=n, scalar_f64=True)
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    shifts = (0, 7919, 104729)
+    calls = []
+    for shift in shifts:
+        got, o = plan.alloc_outputs(F, FEATS)
+        for v in got.values():
+            v.fill_(float("nan"))
+        calls.append((shift, got, o, [_frames(capi, c, n, first=s + shift) for s, c in zip(starts, counts)]))
+    torch.cuda.synchronize()
+    for i, (shift, got, o, xs) in enumerate(calls):  # issued back to back, no host wait between
+        st = streams[i & 1].cuda_stream
+        g.extract_device([t.data_ptr() for t in xs], counts, o, capi.output_mask(o), num_chunks=nch,
+                         streams=[st] * ranks)
+    torch.cuda.synchronize()
+    outs = [(shift, got) for shift, got, _, _ in calls]
+    for shift, got in outs:
+        want = plan.extract_torch(_frames(capi, F, n, first=shift), FEATS)
+        torch.cuda.synchronize()
+        for k in want:
+            a = got[k].view(torch.int32) if got[k].dtype == torch.float32 else got[k].view(torch.int64)
+            b = want[k].view(torch.int32) if want[k].dtype == torch.float32 else want[k].view(torch.int64)
+            assert torch.equal(a, b), (k, shift)
+    g.close()

@@ -5,7 +5,11 @@ bench run, after its clock-settle and warmup launches). With parts > 1 (a step o
 bench is that many launches: mgx_extract_device's parts on two streams), the step spans of
 the matching kernel too: first start to last end of each group of `parts` dispatches, over
 the last k steps -- the figure the bench's per-step HIP events measure.
-usage: prof_summary.py KERNEL_TRACE.csv [k] [name-substring] [parts]"""
+With skip > 0 the last `skip` dispatches are left out first (bench.py's single-stream
+launches after its timed steps), and for extract kernels the launch period of the k
+dispatches before them is printed: (last end - first start) / k -- what bench.py's events
+around its pipelined timed region measure (consecutive launches overlap by the drain).
+usage: prof_summary.py KERNEL_TRACE.csv [k] [name-substring] [parts] [skip]"""
 import csv
 import sys
 from collections import defaultdict
@@ -16,6 +20,7 @@ def main():
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     sub = sys.argv[3] if len(sys.argv) > 3 else ""
     parts = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    skip = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     by = defaultdict(list)
     for row in csv.DictReader(open(path)):
         name = row.get("Kernel_Name", "")
@@ -26,6 +31,14 @@ def main():
     print("%-70s %6s %10s %10s %10s %10s" % ("kernel", "n", "mean_ms", "min_ms", "max_ms", "lastK_mean"))
     for name, v in sorted(by.items(), key=lambda kv: -sum(b - a for a, b in kv[1])):
         v.sort()
+        if skip and "extract_kernel" in name and len(v) > skip:
+            alone = [(b - a) * 1e-6 for a, b in v[-skip:]]
+            v = v[:-skip]
+            w = v[-k * parts:]
+            period = (max(b for _, b in w) - w[0][0]) * 1e-6 / k
+            print("  %s: launch period over the %d timed steps %.4f ms; the %d single-stream launches after "
+                  "them: mean %.4f ms, median %.4f" % (name[:60], k, period, skip, sum(alone) / skip,
+                                                        sorted(alone)[skip // 2]))
         ts = [(b - a) * 1e-6 for a, b in v]  # ns -> ms
         kk = k * parts
         last = ts[-kk:]
