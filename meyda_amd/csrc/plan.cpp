@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -457,6 +458,11 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   for (int i = 15; i < mgx::kBark; ++i) p->sharp_tail += 0.066 * exp(0.171 * (i + 1));  // perceptualSharpness.js:10
   // persistent grid: exactly the workgroups that are resident at once
   p->grid_cap = prop.multiProcessorCount * std::max(1, mgx::extract_blocks_per_cu(n, (int)d->precision, (int)d->mode, (int)d->num_mfcc_coeffs, (int)d->num_mel_bands));
+  // (tuning knob: MGX_GRID_CAP overrides the persistent grid's size; MGX_GRID_CAP=print reports it)
+  if (const char* gc = getenv("MGX_GRID_CAP")) {
+    if (strcmp(gc, "print") == 0) fprintf(stderr, "mgx: grid_cap %d (%d CUs)\n", p->grid_cap, prop.multiProcessorCount);
+    else if (atoi(gc) > 0) p->grid_cap = atoi(gc);
+  }
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),

@@ -7,6 +7,9 @@ C4: 262,144 x N=1024, 40-band mel + 13-coefficient MFCC
 C5: 262,144 x N=2048 per GPU (the 8-GPU config's shard), all features incl. MFCC
 C34-tone: the bench workload (all features, N=1024) on a 440 Hz tone + noise
 Bytes per frame follow SURVEY.md §8(d): 4N in + 4 bytes per output float.
+Each row: back-to-back launches on one stream (kernel_ms, the launch on its own) and the same
+launches pipelined over two streams and two output sets as bench.py runs its steps
+(pipelined_ms, the launch period).
 """
 import json
 import os
@@ -44,6 +47,9 @@ def tone_frames(frames, n):
     frames.mul_(1e-2).add_(sig.to(torch.float32))
 
 
+S2 = []  # the second stream, created once
+
+
 def run(name, cfg, reps=20):
     n, F = cfg["n"], cfg["F"]
     frames = torch.empty(F, n, dtype=torch.float32, device="cuda")
@@ -52,6 +58,7 @@ def run(name, cfg, reps=20):
         tone_frames(frames, n)
     plan = capi.Plan(buffer_size=n, num_mel_bands=cfg["mel"])
     _, o = plan.alloc_outputs(F, cfg["feats"])
+    _, o2 = plan.alloc_outputs(F, cfg["feats"])
     s = torch.cuda.current_stream()
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.15:  # clock settle
@@ -64,10 +71,31 @@ def run(name, cfg, reps=20):
     b.record(s)
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
+    s2 = S2[0] if S2 else S2.append(torch.cuda.Stream()) or S2[0]
+
+    def piped(k):
+        e = torch.cuda.Event()
+        e.record(s)
+        s2.wait_event(e)
+        for i in range(k):
+            st, oo = (s2, o2) if i & 1 else (s, o)
+            plan.extract_device(frames.data_ptr(), F, oo, st.cuda_stream)
+        e = torch.cuda.Event()
+        e.record(s2)
+        s.wait_event(e)
+    piped(8)  # (the first launches on a stream's hardware queue carry a one-time cost of milliseconds)
+    torch.cuda.synchronize()
+    a.record(s)
+    piped(reps)
+    b.record(s)
+    torch.cuda.synchronize()
+    pms = a.elapsed_time(b) / reps
     bpf = 4 * n + 4 * cfg["out_floats"]
     gbs = F * bpf / (ms * 1e-3) / 1e9
     r = {"config": name, "n": n, "frames": F, "features": cfg["feats"], "mel_bands": cfg["mel"], "kernel_ms": ms,
-         "frames_per_s": F / (ms * 1e-3), "bytes_per_frame": bpf, "achieved_GBs": gbs, "hbm_frac": gbs / 8000.0}
+         "frames_per_s": F / (ms * 1e-3), "bytes_per_frame": bpf, "achieved_GBs": gbs, "hbm_frac": gbs / 8000.0,
+         "pipelined_ms": pms, "pipelined_frames_per_s": F / (pms * 1e-3),
+         "pipelined_hbm_frac": F * bpf / (pms * 1e-3) / 1e9 / 8000.0}
     print(json.dumps(r), flush=True)
     return r
 

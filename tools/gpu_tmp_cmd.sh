@@ -2,8 +2,9 @@
 # Scratch GPU command of the current experiment (kept for the record of what ran).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-O=$R/gpurun_out/prof2 && mkdir -p $O
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 100 --warmup 20 --no-cpu-baseline --no-host-path --no-pmc --no-every-output > $O/prof_bench.log 2>&1
-rc=$?; tail -1 $O/prof_bench.log; [ $rc -ne 0 ] && exit $rc
-python3 $R/tools/prof_summary.py $O/prof/run_kernel_trace.csv 100 "" 1 20
+O=$R/gpurun_out/fin && mkdir -p $O && cd $R
+timeout -k 10 300 python tools/configs_bench.py > $O/configs.log 2>&1 || { tail $O/configs.log; exit 1; }
+timeout -k 10 120 python tools/step_overlap.py --rounds 3 --steps 50 > $O/overlap.log 2>&1 || exit 1
+grep median $O/overlap.log
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || { tail $O/bench.log; exit 1; }
+tail -1 $O/bench.log | cut -c1-300
