@@ -170,3 +170,32 @@ def test_loopback_group_calls_overlap_on_two_streams(capi, ranks, nch):
             b = want[k].view(torch.int32) if want[k].dtype == torch.float32 else want[k].view(torch.int64)
             assert torch.equal(a, b), (k, shift)
     g.close()
+
+
+@pytest.mark.parametrize("n", [512, 1024, 2048])
+def test_plan_launches_pipelined_on_two_streams(capi, n):
+    """One plan, consecutive launches alternating between two streams with their own outputs
+    (bench.py's pipelined steps): the launches run concurrently and each record
+    equals the same batch extracted alone, bit for bit."""
+    import torch
+    F = 65536 + 37
+    plan = capi.Plan(buffer_size=n, scalar_f64=True)
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    calls = []
+    for i in range(4):
+        got, o = plan.alloc_outputs(F, FEATS)
+        calls.append((got, o, _frames(capi, F, n, first=i * 1009)))
+    torch.cuda.synchronize()
+    ev = torch.cuda.Event()
+    ev.record(streams[0])
+    streams[1].wait_event(ev)
+    for i, (_, o, x) in enumerate(calls):  # issued back to back
+        plan.extract_device(x.data_ptr(), F, o, streams[i & 1].cuda_stream)
+    torch.cuda.synchronize()
+    for i, (got, _, x) in enumerate(calls):
+        want = plan.extract_torch(x, FEATS)
+        torch.cuda.synchronize()
+        for k in want:
+            a = got[k].view(torch.int32) if got[k].dtype == torch.float32 else got[k].view(torch.int64)
+            b = want[k].view(torch.int32) if want[k].dtype == torch.float32 else want[k].view(torch.int64)
+            assert torch.equal(a, b), (k, i)
