@@ -129,9 +129,20 @@ def capi_seed():
     return meyda_amd.SEED
 
 
+_STREAMS = []
+
+
+def stream_pair():
+    """The two streams every pipelined loop of the run uses, created once: a stream's first
+    launches carry a one-time cost of milliseconds (its hardware queue), which settle() absorbs."""
+    if not _STREAMS:
+        _STREAMS.extend([torch.cuda.current_stream(), torch.cuda.Stream()])
+    return _STREAMS
+
+
 def settle(step, ms, dist=None):
     """Untimed steps for `ms` of wall time (clock ramp-up), before the warmup steps."""
-    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    streams = stream_pair()
     t0 = time.perf_counter()
     go = True
     while go:
@@ -241,7 +252,7 @@ def run_mode(step, steps, warmup, dist):
     steps: an event pair per step cost 1-2 % of the step time, tools/step_overlap.py). Then an
     untimed single-stream pass with an event pair around each launch: the launch duration on
     its own, which is what rocprofv3 reports per dispatch."""
-    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    streams = stream_pair()
     pipelined(step, streams, 0, warmup)
     torch.cuda.synchronize()
     if dist:
