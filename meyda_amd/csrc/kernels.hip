@@ -1623,6 +1623,12 @@ __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
   }
 }
 
+#if MGX_WAVE_TIMES
+// (diagnostic build only, tools/wave_times.py) per wave: start, after the prologue, end (the
+// 100 MHz real-time clock) and the CU id / workgroup
+__device__ unsigned long long g_wave_times[65536 * 4];
+#endif
+
 template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
@@ -1639,6 +1645,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   float2* buf = slot_all + wave * G::SLOT_PHYS;
   FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off) + wave * FPW;  // this wave's records
   KArgs* ap = args_ptr();
+#if MGX_WAVE_TIMES
+  const unsigned long long wt0 = wall_clock64();
+#endif
 
   // Kernel constants and the DCT table, once per workgroup (the only workgroup barrier).
   {
@@ -1656,6 +1665,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     for (int i = threadIdx.x; i < ntp; i += kThreads) dct_lds[i] = i < nt ? dct[i] : 0.0f;
   }
   lds_barrier();
+#if MGX_WAVE_TIMES
+  const unsigned long long wt1 = wall_clock64();
+#endif
 
   int lp[G::NPASS];
 #pragma unroll
@@ -1861,6 +1873,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     MGX_MARK(phase2_end);
     wave_sync();  // records and slot buffer are reused by the next batch
   }
+#if MGX_WAVE_TIMES
+  if (lane == 0 && blockIdx.x < 16384) {
+    auto g = (__attribute__((address_space(1))) unsigned long long*)g_wave_times + ((uint64_t)blockIdx.x * 4 + wave) * 4;
+    g[0] = wt0;
+    g[1] = wt1;
+    g[2] = wall_clock64();
+    g[3] = __smid() | ((uint64_t)blockIdx.x << 32);
+  }
+#endif
 }
 
 __global__ void synth_kernel(float* __restrict__ out, uint64_t count, uint64_t seed, uint64_t first) {
@@ -2043,3 +2064,9 @@ hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t firs
 }
 
 }  // namespace mgx
+
+#if MGX_WAVE_TIMES
+extern "C" int mgx_debug_wave_times(unsigned long long* host, int count) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mgx::g_wave_times), (size_t)count * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
