@@ -58,7 +58,25 @@ def main():
         e2.record(s1)
         s0.wait_event(e2)
 
-    modes = {"events": events, "plain": plain, "two_streams": two_streams}
+    H = F // 2
+    _, oa = plan.alloc_outputs(H, capi.ALL_FEATURES)
+    _, ob = plan.alloc_outputs(F - H, capi.ALL_FEATURES)
+    xb = x[H:]
+
+    def split2():
+        # one step = two half launches on the two streams, joined at the step's end (what an
+        # internal split of one call would do)
+        for _ in range(K):
+            e = torch.cuda.Event()
+            e.record(s0)
+            s1.wait_event(e)
+            plan.extract_device(x.data_ptr(), H, oa, s0.cuda_stream)
+            plan.extract_device(xb.data_ptr(), F - H, ob, s1.cuda_stream)
+            e2 = torch.cuda.Event()
+            e2.record(s1)
+            s0.wait_event(e2)
+
+    modes = {"events": events, "plain": plain, "two_streams": two_streams, "split2": split2}
     res = {m: [] for m in modes}
     for m in modes.values():  # warm up every mode (clock settle)
         for _ in range(3):
