@@ -1604,6 +1604,14 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   return sc == MGX_RMS ? sqrt_d(v) : sc == MGX_PERCEPTUAL_SPREAD ? v * v : v;
 }
 
+// Work shares of the four workgroup ranks of a CU at N = 1024 (sum 64; extract_kernel).
+#ifndef MGX_SHARE0
+#define MGX_SHARE0 22
+#define MGX_SHARE1 17
+#define MGX_SHARE2 14
+#define MGX_SHARE3 11
+#endif
+
 // Copy of the TwLds image from the plan tables, once per workgroup (before its LDS barrier).
 template <int N, int P, int I>
 __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
@@ -1689,8 +1697,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // consecutive: a workgroup fills whole 64/128-byte lines of every scalar output in its
   // own XCD's L2 instead of sharing each line with a workgroup on another XCD.
   const uint64_t wstride = 4;
-  const uint64_t ng = (nb + 3) / 4, per = (ng + gridDim.x - 1) / gridDim.x;
-  const uint64_t g0 = (uint64_t)blockIdx.x * per, g1 = g0 + per < ng ? g0 + per : ng;
+  // The shares are not equal at N = 1024: the four workgroups of a CU are dispatched in
+  // blockIdx order (rank r = blockIdx / (grid / 4) on every CU), and at equal priority the
+  // SIMD's arbiter favours the oldest wave, so with equal shares rank 0 finished at 64 % of
+  // the launch and the SIMDs ran 3, 2, then 1 wave for the rest (tools/wave_times.py).
+  // Rank r takes MGX_SHARE_r / 64 of the groups instead.
+  const uint64_t ng = (nb + 3) / 4;
+  uint64_t g0, g1;
+  if (N == 1024 && ap->wg_ranks == 4 && (gridDim.x & 3) == 0) {
+    constexpr uint64_t c1 = MGX_SHARE0, c2 = c1 + MGX_SHARE1, c3 = c2 + MGX_SHARE2, cs = c3 + MGX_SHARE3;
+    const uint64_t q = gridDim.x / 4, r = blockIdx.x / q, i = blockIdx.x % q;
+    const uint64_t ca = r == 0 ? 0 : r == 1 ? c1 : r == 2 ? c2 : c3, cb = r == 0 ? c1 : r == 1 ? c2 : r == 2 ? c3 : cs;
+    const uint64_t lo = ng * ca / cs, hi = ng * cb / cs, per = (hi - lo + q - 1) / q;
+    g0 = lo + i * per < hi ? lo + i * per : hi;
+    g1 = g0 + per < hi ? g0 + per : hi;
+  } else {
+    const uint64_t per = (ng + gridDim.x - 1) / gridDim.x;
+    g0 = (uint64_t)blockIdx.x * per;
+    g0 = g0 < ng ? g0 : ng;
+    g1 = g0 + per < ng ? g0 + per : ng;
+  }
   const uint64_t b0 = g0 * 4 + wave, bend = g1 * 4 < nb ? g1 * 4 : nb;
   // Loads are unconditional (the frame index is clamped; results of frames past the end
   // are never stored), so they issue back to back with no branches or waits between them.

@@ -52,6 +52,7 @@ struct KernelArgs {
   int dct_sequential;    // MGX_FLAG_DCT_SEQUENTIAL: the DCT as VALU FMAs in the reference's order
   int mfcc_reference;    // MGX_FLAG_MFCC_REFERENCE: mel sums, log and DCT in the reference's order (SUB kernel)
   int mel_zero;          // some mel segment [b_m, b_{m+1}) is empty: the scan's slots are zeroed first
+  int wg_ranks;          // workgroups per CU when the grid is the resident one (else 1): their work shares
 };
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.

@@ -322,6 +322,7 @@ struct mgx_plan {
   mgx::DevTables t{};
   double freq_sum = 0, pow_freq_sum = 0, nyq = 0, sharp_tail = 0;
   int grid_cap = 1;
+  int cus = 0;  // compute units of the plan's device
   int mel_zero = 1;  // some mel segment is empty (kernels.hip mel_energies)
   // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
   float* s_frames[2] = {nullptr, nullptr};
@@ -458,6 +459,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   for (int i = 15; i < mgx::kBark; ++i) p->sharp_tail += 0.066 * exp(0.171 * (i + 1));  // perceptualSharpness.js:10
   // persistent grid: exactly the workgroups that are resident at once
   p->grid_cap = prop.multiProcessorCount * std::max(1, mgx::extract_blocks_per_cu(n, (int)d->precision, (int)d->mode, (int)d->num_mfcc_coeffs, (int)d->num_mel_bands));
+  p->cus = prop.multiProcessorCount;
   // (tuning knob: MGX_GRID_CAP overrides the persistent grid's size; MGX_GRID_CAP=print reports it)
   if (const char* gc = getenv("MGX_GRID_CAP")) {
     if (strcmp(gc, "print") == 0) fprintf(stderr, "mgx: grid_cap %d (%d CUs)\n", p->grid_cap, prop.multiProcessorCount);
@@ -563,6 +565,7 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   const uint64_t fb = (uint64_t)mgx::frames_per_batch(p->n);
   const uint64_t nb = (nframes + fb - 1) / fb;
   const int grid = (int)std::min<uint64_t>(nb, (uint64_t)p->grid_cap);
+  a.wg_ranks = grid == p->grid_cap && p->cus > 0 ? p->grid_cap / p->cus : 1;
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream);

@@ -2,8 +2,11 @@
 # Scratch GPU command of the current experiment (kept for the record of what ran).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-O=$R/gpurun_out/pool3 && mkdir -p $O && cd $R
-for r in 1 2; do for v in tg0 tg3 tg4; do
-  MEYDA_AMD_LIB=$R/abl/libabl_$v.so timeout -k 10 200 python bench.py --no-cpu-baseline --no-host-path --no-pmc --no-every-output > $O/b_$v.log 2>&1 || { tail $O/b_$v.log; exit 1; }
-  tail -1 $O/b_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$v', round(d['value']/1e6,1), round(d['ms_per_step'],4), 'alone', round(r['step_event_ms']['launch_alone_median_ms'],4))"
-done; done
+O=$R/gpurun_out/shares3 && mkdir -p $O && cd $R
+bash tools/gpu_check.sh all > $O/check.log 2>&1
+rc=$?; tail -2 $O/check.log; [ $rc -ne 0 ] && exit $rc
+C3=spectralCentroid,spectralFlatness,spectralSlope,spectralRolloff,spectralSpread,spectralSkewness,spectralKurtosis,loudness,perceptualSpread,perceptualSharpness
+timeout -k 10 200 python tools/ab_libs.py --rounds 5 --features $C3 eq=abl/libabl_eq.so base=base > $O/c3.log 2>&1 || exit 1
+echo C3; grep median $O/c3.log
+timeout -k 10 200 python tools/ab_libs.py --rounds 5 --features mfcc eq=abl/libabl_eq.so base=base > $O/c4.log 2>&1 || exit 1
+echo mfcc; grep median $O/c4.log

@@ -63,6 +63,10 @@ def main():
     for k in range(8):
         m = xcd == k
         print("XCD %d (wg %% 8): waves %d  end mean %.1f  min %.1f  max %.1f us" % (k, m.sum(), us(t2[m]).mean(), us(t2[m]).min(), us(t2[m]).max()))
+    # which waves finish first: by workgroup rank groups and by the wave's index in its workgroup
+    ng = len(np.unique(wg))
+    for name, key in (("wg // (grid/4)", wg // max(1, ng // 4)), ("wg % 4", wg % 4), ("wave in wg", np.arange(len(wg)) % 4)):
+        print("end by %-15s: %s" % (name, "  ".join("%d:%.0f" % (k, us(t2[key == k]).mean()) for k in np.unique(key)[:8])))
     # resident waves over time: what fraction of the 16 slots per CU x 256 CUs is alive
     grid = np.linspace(0, span, 41)
     alive = [((us(t0) <= g) & (us(t2) > g)).sum() for g in grid]
