@@ -1605,6 +1605,9 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
 }
 
 // Work shares of the four workgroup ranks of a CU at N = 1024 (sum 64; extract_kernel).
+#ifndef MGX_RANK_SHARES
+#define MGX_RANK_SHARES 1  // the other N: linear 2:1 rank weights
+#endif
 #ifndef MGX_SHARE0
 #define MGX_SHARE0 22
 #define MGX_SHARE1 17
@@ -1704,7 +1707,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // Rank r takes MGX_SHARE_r / 64 of the groups instead.
   const uint64_t ng = (nb + 3) / 4;
   uint64_t g0, g1;
-  if (N == 1024 && ap->wg_ranks == 4 && (gridDim.x & 3) == 0) {
+  const uint64_t nr = (uint64_t)ap->wg_ranks;
+  // (unequal shares need many groups per workgroup: with a few each, their rounding unbalances
+  // more than the ranks' rates do -- C2's 65,536 frames at N = 512 lost 6 %; and N = 256 lost 4 %)
+  const bool many = ng >= 8 * (uint64_t)gridDim.x;
+  if (N >= 512 && N != 1024 && MGX_RANK_SHARES && many && nr >= 2 && nr <= 8 && gridDim.x % nr == 0) {
+    // other N: rank r's weight 2 (R - 1) - r, from 2:1 for the first rank to the last
+    const uint64_t q = gridDim.x / nr, r = blockIdx.x / q, i = blockIdx.x % q;
+    auto cum = [&](uint64_t k) { return k * 2 * (nr - 1) - k * (k - 1) / 2; };
+    const uint64_t cs = cum(nr), lo = ng * cum(r) / cs, hi = ng * cum(r + 1) / cs, per = (hi - lo + q - 1) / q;
+    g0 = lo + i * per < hi ? lo + i * per : hi;
+    g1 = g0 + per < hi ? g0 + per : hi;
+  } else if (N == 1024 && many && nr == 4 && (gridDim.x & 3) == 0) {
     constexpr uint64_t c1 = MGX_SHARE0, c2 = c1 + MGX_SHARE1, c3 = c2 + MGX_SHARE2, cs = c3 + MGX_SHARE3;
     const uint64_t q = gridDim.x / 4, r = blockIdx.x / q, i = blockIdx.x % q;
     const uint64_t ca = r == 0 ? 0 : r == 1 ? c1 : r == 2 ? c2 : c3, cb = r == 0 ? c1 : r == 1 ? c2 : r == 2 ? c3 : cs;
