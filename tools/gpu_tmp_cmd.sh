@@ -2,12 +2,17 @@
 # Scratch GPU command of the current experiment (kept for the record of what ran).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-O=$R/gpurun_out/shares5 && mkdir -p $O && cd $R
-bash tools/gpu_check.sh all > $O/check.log 2>&1
-rc=$?; tail -1 $O/check.log; [ $rc -ne 0 ] && exit $rc
-for n in 256 512 1024 2048; do
-  timeout -k 10 200 python tools/ab_libs.py --n $n --rounds 5 --compare r0=abl/libabl_eq.so base=base > $O/n$n.log 2>&1 || { tail $O/n$n.log; exit 1; }
-  echo "N=$n"; grep -E "median|outputs" $O/n$n.log
+O=$R/gpurun_out/shares6 && mkdir -p $O && cd $R
+for r in 1 2; do for v in eq base; do
+  L=$R/abl/libabl_$v.so; [ $v = base ] && L=$R/meyda_amd/libmeyda_gpu.so
+  MEYDA_AMD_LIB=$L timeout -k 10 200 python bench.py --no-cpu-baseline --no-host-path --no-pmc --no-every-output > $O/b_$v.log 2>&1 || { tail $O/b_$v.log; exit 1; }
+  tail -1 $O/b_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$v', round(d['value']/1e6,1), round(d['ms_per_step'],4), 'alone', round(r['step_event_ms']['launch_alone_median_ms'],4))"
+done; done
+for v in eq base; do
+  L=$R/abl/libabl_$v.so; [ $v = base ] && L=$R/meyda_amd/libmeyda_gpu.so
+  MEYDA_AMD_LIB=$L timeout -k 10 200 python tools/configs_bench.py C5 C3 > $O/c_$v.log 2>&1 || exit 1
+  echo "== $v"; grep '^{' $O/c_$v.log | python3 -c "
+import sys,json
+for l in sys.stdin:
+    c=json.loads(l); print(c['config'], 'alone', round(c['kernel_ms'],4), 'piped', round(c['pipelined_ms'],4))"
 done
-timeout -k 10 200 python tools/ab_libs.py --n 512 --frames 65536 --features amplitudeSpectrum,spectralCentroid --rounds 5 r0=abl/libabl_eq.so base=base > $O/c2.log 2>&1 || exit 1
-echo C2; grep median $O/c2.log
