@@ -1606,7 +1606,10 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
 
 // Work shares of the four workgroup ranks of a CU at N = 1024 (sum 64; extract_kernel).
 #ifndef MGX_RANK_SHARES
-#define MGX_RANK_SHARES 1  // the other N: linear 2:1 rank weights
+#define MGX_RANK_SHARES 1  // the other N: linear rank weights A (R - 1) - r
+#endif
+#ifndef MGX_RANK_A
+#define MGX_RANK_A 2  // A = 2: 2:1 from the first rank to the last; 3: 1.5:1
 #endif
 #ifndef MGX_SHARE0
 #define MGX_SHARE0 22
@@ -1714,7 +1717,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   if (N >= 512 && N != 1024 && MGX_RANK_SHARES && many && nr >= 2 && nr <= 8 && gridDim.x % nr == 0) {
     // other N: rank r's weight 2 (R - 1) - r, from 2:1 for the first rank to the last
     const uint64_t q = gridDim.x / nr, r = blockIdx.x / q, i = blockIdx.x % q;
-    auto cum = [&](uint64_t k) { return k * 2 * (nr - 1) - k * (k - 1) / 2; };
+    auto cum = [&](uint64_t k) { return k * MGX_RANK_A * (nr - 1) - k * (k - 1) / 2; };
     const uint64_t cs = cum(nr), lo = ng * cum(r) / cs, hi = ng * cum(r + 1) / cs, per = (hi - lo + q - 1) / q;
     g0 = lo + i * per < hi ? lo + i * per : hi;
     g1 = g0 + per < hi ? g0 + per : hi;
