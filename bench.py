@@ -13,14 +13,18 @@ Inputs are generated in HBM before the timed region. Consecutive steps alternate
 between two streams and two output sets, as a caller streaming batches runs them: one
 launch's drain (its last waves leaving the SIMDs) overlaps the next launch's start.
 
-Multi-GPU (torchrun, one process per GPU): each rank extracts its own 262,144-frame
-shard of one global stream (weak scaling) through the library's multi-device group
-(include/meyda_gpu.h, mgx_group_create_rank), which gathers every rank's per-frame
-feature records to rank 0 over xGMI with RCCL point-to-point transfers, chunked so
-that chunk i's transfer overlaps chunk i+1's extraction (the north star's gather is
-inside the timed step; --no-gather times the shards alone). torch.distributed (gloo)
-is only the control plane: the RCCL id broadcast, barriers and the max-over-ranks
-elapsed time. Rank 0 prints the JSON line with the whole-job frames/s.
+Multi-GPU (--gpus N): one process per GPU under torchrun (the driver's launch; --gpus must
+equal WORLD_SIZE), or one process driving devices 0..N-1 without it; never fewer GPUs than
+asked (the run fails instead). Each rank extracts its own 262,144-frame shard of one global
+stream (weak scaling). The run is measured twice: the shards alone, then the steps through
+the library's multi-device group (include/meyda_gpu.h, mgx_group_create_rank /
+mgx_group_create), which gathers every rank's per-frame feature records to rank 0 over
+xGMI with RCCL point-to-point transfers, chunked so that chunk i's transfer overlaps chunk
+i+1's extraction. `value` is the gather-inclusive rate (the north star's gather inside the
+timed step); if the gather fails or passes its deadline, rank 0 reports the shards with the
+gather's status instead. The RCCL communicator's own view (ranks, rank, device) and every
+rank's GPU (uuid, PCI bus) are in the line. torch.distributed (gloo) is only the control
+plane: the RCCL id broadcast, barriers and the max-over-ranks elapsed time.
 """
 import argparse
 import concurrent.futures as cf
@@ -44,7 +48,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of the job (default: the torchrun world size, else 1). Under torchrun it must equal "
+                         "WORLD_SIZE; without torchrun, N > 1 drives devices 0..N-1 from this one process")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--settle-ms", type=float, default=150.0,
@@ -57,10 +63,16 @@ def parse():
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     ap.add_argument("--cpu-seconds", type=float, default=6.0,
                     help="CPU baseline: seconds of the multi-thread run (1 thread and the C port: a third)")
-    ap.add_argument("--also-fast", action="store_true", help="report the fp32 mode alongside")
+    ap.add_argument("--no-fast", action="store_true", help="N = 1: skip the fp32-butterfly mode beside the faithful one")
+    ap.add_argument("--no-c3", action="store_true", help="N = 1: skip the config C3 feature set (spectral* + loudness)")
+    ap.add_argument("--no-c4", action="store_true", help="N = 1: skip config C4 exactly (40 mel bands, 13 MFCC)")
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: time the shards alone, without the RCCL gather to rank 0")
     ap.add_argument("--chunks", type=int, default=0, help="N > 1: gather pipeline depth (0 = automatic)")
+    ap.add_argument("--gather-timeout", type=float, default=180.0,
+                    help="N > 1: deadline (s) of the gather phase; past it rank 0 reports the shards alone")
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="rehearsal only: ranks may share a GPU (RCCL refuses that, so no gather)")
     ap.add_argument("--no-every-output", action="store_true",
                     help="N = 1: skip the secondary timing with every output (spectra too) and 40 mel bands")
     ap.add_argument("--no-pmc", action="store_true",
@@ -129,46 +141,57 @@ def capi_seed():
     return meyda_amd.SEED
 
 
-_STREAMS = []
+class Devices:
+    """The devices this process drives (one under torchrun; N for a single-process --gpus N
+    run), each with the two streams every pipelined loop of the run uses, created once: a
+    stream's first launches carry a one-time cost of milliseconds (its hardware queue), which
+    settle() absorbs."""
+
+    def __init__(self, devs):
+        self.devs = list(devs)
+        self.streams = {}
+        for d in self.devs:
+            with torch.cuda.device(d):
+                self.streams[d] = [torch.cuda.current_stream(d), torch.cuda.Stream(device=d)]
+
+    def stream(self, d, k):
+        return self.streams[d][k & 1]
+
+    def sync(self):
+        for d in self.devs:
+            torch.cuda.synchronize(d)
 
 
-def stream_pair():
-    """The two streams every pipelined loop of the run uses, created once: a stream's first
-    launches carry a one-time cost of milliseconds (its hardware queue), which settle() absorbs."""
-    if not _STREAMS:
-        _STREAMS.extend([torch.cuda.current_stream(), torch.cuda.Stream()])
-    return _STREAMS
+def pipelined(step, devs, first, count):
+    """Steps first..first+count-1, consecutive steps alternating between each device's two
+    streams and two output sets (step(k) launches step k on stream k & 1 of every local
+    device): a stream of batches the way a streaming caller runs it, so step i+1's workgroups
+    start on the CUs step i's last waves leave while it drains (one launch ends with ~45 us of
+    SIMDs running out of waves). Forks from and joins back into stream 0."""
+    for d in devs.devs:
+        e = torch.cuda.Event()
+        e.record(devs.stream(d, 0))
+        devs.stream(d, 1).wait_event(e)
+    for i in range(first, first + count):
+        step(i)
+    for d in devs.devs:
+        e = torch.cuda.Event()
+        e.record(devs.stream(d, 1))
+        devs.stream(d, 0).wait_event(e)
 
 
-def settle(step, ms, dist=None):
+def settle(step, devs, ms, dist=None):
     """Untimed steps for `ms` of wall time (clock ramp-up), before the warmup steps."""
-    streams = stream_pair()
     t0 = time.perf_counter()
     go = True
     while go:
-        pipelined(step, streams, 0, 8)
-        torch.cuda.synchronize()
+        pipelined(step, devs, 0, 8)
+        devs.sync()
         go = (time.perf_counter() - t0) * 1e3 < ms
         if dist:  # every rank runs the same number of (collective) steps
             t = torch.tensor([1 if go else 0], dtype=torch.int32)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             go = bool(t.item())
-
-
-def pipelined(step, streams, first, count):
-    """Steps first..first+count-1, consecutive steps alternating between the two streams and
-    the two output sets (step(stream, k), k = i & 1): a stream of batches the way a streaming
-    caller runs it, so step i+1's workgroups start on the CUs step i's last waves leave while it
-    drains (one launch ends with ~45 us of SIMDs running out of waves). Forks
-    from and joins back into streams[0]."""
-    e = torch.cuda.Event()
-    e.record(streams[0])
-    streams[1].wait_event(e)
-    for i in range(first, first + count):
-        step(streams[i & 1].cuda_stream, i & 1)
-    e = torch.cuda.Event()
-    e.record(streams[1])
-    streams[0].wait_event(e)
 
 
 def host_path(plan, frames, reps=3):
@@ -245,25 +268,26 @@ def pmc_live(n, F, precision):
     return read + write, valu, note
 
 
-def run_mode(step, steps, warmup, dist):
+def run_mode(step, devs, steps, warmup, dist):
     """W untimed steps, then exactly `steps` timed ones bracketed by a barrier and a device
     synchronisation on both sides, pipelined over two streams (pipelined()); HIP events on the
     launch stream around the whole timed region give the launch period (no events between the
     steps: an event pair per step cost 1-2 % of the step time, tools/step_overlap.py). Then an
     untimed single-stream pass with an event pair around each launch: the launch duration on
     its own, which is what rocprofv3 reports per dispatch."""
-    streams = stream_pair()
-    pipelined(step, streams, 0, warmup)
-    torch.cuda.synchronize()
+    d0 = devs.devs[0]
+    s0 = devs.stream(d0, 0)
+    pipelined(step, devs, 0, warmup)
+    devs.sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    devs.sync()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    e0.record(streams[0])
-    pipelined(step, streams, 0, steps)
-    e1.record(streams[0])
-    torch.cuda.synchronize()
+    e0.record(s0)
+    pipelined(step, devs, 0, steps)
+    e1.record(s0)
+    devs.sync()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -271,10 +295,10 @@ def run_mode(step, steps, warmup, dist):
     # the launch on its own (serialised on one stream), untimed by the step clock
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
     for a, b in ev:
-        a.record(streams[0])
-        step(streams[0].cuda_stream, 0)
-        b.record(streams[0])
-    torch.cuda.synchronize()
+        a.record(s0)
+        step(0)  # every local device's stream 0: serialised behind the previous launch
+        b.record(s0)
+    devs.sync()
     iso = [a.elapsed_time(b) for a, b in ev]
     stats = {"period_ms": period, "launch_alone_mean_ms": float(np.mean(iso)),
              "launch_alone_median_ms": float(np.median(iso)), "launch_alone_min_ms": float(np.min(iso)),
@@ -291,138 +315,281 @@ def run_mode(step, steps, warmup, dist):
     return elapsed, period, stats
 
 
+def resolve_topology(gpus, env, ndev, allow_shared=False):
+    """How this run maps onto GPUs; fails loudly (SystemExit) instead of measuring fewer GPUs
+    than asked. Under torchrun (WORLD_SIZE set) --gpus must equal the world size and every
+    local rank needs a GPU of its own (--allow-shared-gpu: a rehearsal only). Without torchrun
+    --gpus N > 1 drives devices 0..N-1 from this one process. Returns (mode, gpus), mode one
+    of "torchrun", "single" (one process, N devices) or "one"."""
+    from meyda_amd import dist as mdist
+    _, _, world = mdist.env_rank_world(env)
+    if "WORLD_SIZE" in env:
+        gpus = world if gpus is None else gpus
+        if gpus != world:
+            raise SystemExit("bench.py: --gpus %d but the launcher started %d ranks (WORLD_SIZE)" % (gpus, world))
+        local_world = int(env.get("LOCAL_WORLD_SIZE", world))
+        if ndev < local_world and not allow_shared:
+            raise SystemExit("bench.py: %d ranks on this node but %d GPU(s) visible (one GPU per rank; "
+                             "--allow-shared-gpu for a rehearsal)" % (local_world, ndev))
+        return ("torchrun" if world > 1 else "one"), gpus
+    gpus = 1 if gpus is None else gpus
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if gpus > ndev:
+        raise SystemExit("bench.py: --gpus %d but %d GPU(s) visible" % (gpus, ndev))
+    return ("single" if gpus > 1 else "one"), gpus
+
+
+class Watchdog:
+    """Deadline of the gather phase of a multi-GPU run. The RCCL path cannot be interrupted
+    once a peer is missing (a rank that failed, a message never posted), so when the deadline
+    passes rank 0 prints the line it already has -- the shards measured without the gather,
+    with the gather's status -- and every rank leaves (exit 0, so the launcher does not tear
+    rank 0 down before it has printed)."""
+
+    def __init__(self, seconds, emit):
+        import threading
+        self.emit = emit
+        self.t = threading.Timer(seconds, self._fire)
+        self.t.daemon = True
+        self.t.start()
+
+    def _fire(self):
+        try:
+            self.emit("timed out")
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+
+    def cancel(self):
+        self.t.cancel()
+
+
 def main():
     args = parse()
     from meyda_amd import dist as mdist
+    mode, gpus = resolve_topology(args.gpus, os.environ, torch.cuda.device_count(), args.allow_shared_gpu)
     rank, local, world = mdist.env_rank_world()
     dist = None
-    # one GPU per rank; (a box with fewer GPUs than ranks, a rehearsal only, shares them)
-    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-    if world > 1:
+    if mode == "torchrun":
         import torch.distributed as tdist
-        mdist.init("gloo")  # control plane only; the data path is the library's RCCL gather
+        mdist.init_control_plane()  # gloo: control plane only; the data path is the library's RCCL gather
         dist = tdist
-    n, F = args.n, args.frames
-    frames = torch.empty(F, n, dtype=torch.float32, device="cuda")
-    # each rank its own shard of one global synthetic stream
-    capi.synth_frames_device(frames, capi_seed(), first_frame=rank * F)
-    dev = torch.cuda.current_device()
-    plan = capi.Plan(buffer_size=n, precision=args.precision, device=dev)
-    gather = world > 1 and not args.no_gather
-    if gather:
-        uid = [capi.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        group = capi.Group(buffer_size=n, rank=rank, nranks=world, unique_id=uid[0], precision=args.precision,
-                           device=dev)
-        # rank 0 holds the whole job's feature record; the other ranks only their transfer buffers
-        # (two output sets: consecutive steps are in flight together, pipelined())
-        sets = [plan.alloc_outputs(F * world if rank == 0 else 1, FEATURES) for _ in range(2)]
-        mask = capi.output_mask(sets[0][1])
-
-        def step(s, k):
-            group.extract_device([frames.data_ptr()], [F] * world, sets[k][1] if rank == 0 else None, mask,
-                                 args.chunks, [s])
+        devs = Devices([local % torch.cuda.device_count()])
     else:
-        sets = [plan.alloc_outputs(F, FEATURES) for _ in range(2)]
+        devs = Devices(range(gpus))
+    torch.cuda.set_device(devs.devs[0])
+    # which GPU every rank / local device is (the driver's node: one each)
+    me = [{"rank": rank + i, "device": d, "uuid": str(torch.cuda.get_device_properties(d).uuid),
+           "pci_bus_id": torch.cuda.get_device_properties(d).pci_bus_id} for i, d in enumerate(devs.devs)]
+    if dist:
+        allr = [None] * world
+        dist.all_gather_object(allr, me)
+        placement = [x for r in allr for x in r]
+    else:
+        placement = me
+    shared = len({p["uuid"] for p in placement}) != len(placement)
+    if shared and not args.allow_shared_gpu:
+        raise SystemExit("bench.py: ranks share a GPU: %s" % placement)
+    n, F = args.n, args.frames
+    # each rank / device its own shard of one global synthetic stream
+    first = rank if dist else 0
+    frames, plans = {}, {}
+    for i, d in enumerate(devs.devs):
+        with torch.cuda.device(d):
+            frames[d] = torch.empty(F, n, dtype=torch.float32, device="cuda:%d" % d)
+            capi.synth_frames_device(frames[d], capi_seed(), first_frame=(first + i) * F)
+            plans[d] = capi.Plan(buffer_size=n, precision=args.precision, device=d)
+    plan, d0 = plans[devs.devs[0]], devs.devs[0]
+    # the shards alone: every local device extracts its own shard (no data-path collective)
+    shard_sets = {d: [plans[d].alloc_outputs(F, FEATURES, device="cuda:%d" % d) for _ in range(2)] for d in devs.devs}
 
-        def step(s, k):
-            plan.extract_device(frames.data_ptr(), F, sets[k][1], s)
-    torch.cuda.synchronize()
-    settle(step, args.settle_ms, dist)
-    elapsed, kernel_ms, step_stats = run_mode(step, args.steps, args.warmup, dist)
-    fast = None
-    if args.also_fast and args.precision != "fast" and world == 1:
-        plan_f = capi.Plan(buffer_size=n, precision="fast", device=dev)
+    def step_shards(k):
+        for d in devs.devs:
+            plans[d].extract_device(frames[d].data_ptr(), F, shard_sets[d][k & 1][1], devs.stream(d, k).cuda_stream)
+    devs.sync()
+    settle(step_shards, devs, args.settle_ms, dist)
+    el_s, km_s, stats_s = run_mode(step_shards, devs, args.steps, args.warmup, dist)
+    value_s = gpus * F * args.steps / el_s
+    gather = None
+    if gpus > 1 and not args.no_gather and not shared:
+        gather = {"status": "not run", "chunks": args.chunks or "auto"}
+    line_box = {}
 
-        def step_f(s, k):
-            plan_f.extract_device(frames.data_ptr(), F, sets[k][1], s)
-        settle(step_f, args.settle_ms)
-        el_f, km_f, _ = run_mode(step_f, args.steps, args.warmup, dist)
-        fast = {"value": world * F * args.steps / el_f, "kernel_ms": km_f,
-                "roofline_frac": (F * (4 * n + 4 * OUT_FLOATS)) / (km_f * 1e-3) / 1e9 / HBM_PEAK_GBS}
-    every = None
-    if world == 1 and not args.no_every_output:
-        # Secondary (never `value`): EVERY output of the path — the headline set plus the
-        # amplitude, power and complex spectra — with the 40-band mel of config C4, same frames
-        plan_e = capi.Plan(buffer_size=n, precision=args.precision, num_mel_bands=40, device=dev)
-        feats_e = FEATURES + ["amplitudeSpectrum", "powerSpectrum", "complexSpectrum"]
-        sets_e = [plan_e.alloc_outputs(F, feats_e) for _ in range(2)]
+    def emit_line(gather_status=None):
+        """Rank 0's JSON line from what has been measured so far."""
+        if rank != 0:
+            return
+        if gather is not None and gather_status is not None:
+            gather["status"] = gather_status
+        print(json.dumps(build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, gather,
+                                    line_box)), flush=True)
 
-        def step_e(s, k):
-            plan_e.extract_device(frames.data_ptr(), F, sets_e[k][1], s)
-        settle(step_e, args.settle_ms)
-        el_e, km_e, _ = run_mode(step_e, args.steps, args.warmup, dist)
-        bpf_e = 4 * n + 4 * (OUT_FLOATS + 2 * (n // 2) + 2 * n)
-        every = {"features": feats_e, "mel_bands": 40, "value": F * args.steps / el_e, "unit": "frames/s",
-                 "kernel_ms": km_e, "bytes_per_frame": bpf_e,
-                 "roofline_frac": F * bpf_e / (km_e * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        del sets_e
-    if rank == 0:
-        bytes_per_frame = 4 * n + 4 * OUT_FLOATS
-        alone_ms = (step_stats["rank0"] if dist else step_stats)["launch_alone_median_ms"]
-        achieved = F * bytes_per_frame / (kernel_ms * 1e-3) / 1e9
-        traffic, valu, traffic_note = None, None, "not measured (--no-pmc or N > 1)"
-        if world == 1 and not args.no_pmc:
-            try:
-                traffic, valu, traffic_note = pmc_live(n, F, args.precision)
-            except Exception as e:  # the counters are a report, never the measurement itself
-                traffic, valu, traffic_note = None, None, "rocprofv3 passes failed: %r" % (e,)
-        if valu is not None:
-            # the faithful path is FP64-VALU bound. Issue costs per wave64
-            # instruction measured by tools/ubench/op_rates.hip (profiles/r01_op_rates.log):
-            # f64 ~5.0, f32<->f64 conversion 4.2 cycles; at the clock this run's kernel time implies
-            cyc = kernel_ms * 1e-3 * 2.4e9 * 1024 / F  # SIMD cycles per frame (2.4 GHz held, 1,024 SIMDs)
-            valu["frame_simd_cycles"] = cyc
-            valu["est_fp64_cvt_busy"] = (valu["f64_per_frame"] * 5.0 + valu["cvt_per_frame"] * 4.2) / cyc
-            # FP64 pipe (vector and matrix share it): 78.6 TFLOP/s dense on MI355X (1,024 SIMDs x 32
-            # FLOP/clk x 2.4 GHz; v_mfma_f64_4x4x4 issues every 16 cycles: tools/ubench/op_rates.hip)
-            mf = valu["mfma_f64"]
-            mf["tflops"] = mf["flop_per_launch"] / (kernel_ms * 1e-3) / 1e12
-            mf["peak_tflops"] = 78.6
-            mf["frac"] = mf["tflops"] / mf["peak_tflops"]
-        line = {
-            "metric": "audio frames/sec (bufferSize=1024, all features) at 1/2/4/8 GPUs; % HBM roofline",
-            "value": world * F * args.steps / elapsed,
-            "unit": "frames/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64 butterflies / f32 storage" if args.precision == "faithful" else "f32",
-            "data": "synthetic (seeded splitmix64 PCM generated in HBM)",
-            "config": {"workload": "C3+C4 all features: %d frames x bufferSize=%d per GPU, float32 outputs" % (F, n),
-                       "buffer_size": n, "frames_per_gpu": F, "features": FEATURES,
-                       "mel_bands": 26, "mfcc_coeffs": 13,
-                       "precision": args.precision, "parallelism": "frame shards, %d proc" % world,
-                       "gather_to_rank0": bool(gather),
-                       "gather": ("RCCL send/recv to rank 0 in the timed step, %s chunks" % (args.chunks or "auto"))
-                       if gather else None},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
-                         "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
-                         "kernel_ms_source": "launch period: HIP events around the timed region / steps "
-                                             "(steps pipelined over two streams); a launch on its own: step_event_ms",
-                         "frac_launch_alone": F * bytes_per_frame / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "step_event_ms": step_stats,
-                         "bytes_per_frame": bytes_per_frame},
-        }
-        if valu:
-            line["valu"] = valu
-        if fast:
-            line["fast_mode"] = fast
-        if every:
-            line["every_output"] = every
-        if world == 1 and not args.no_host_path:
-            line["host_path"] = host_path(plan, frames)
-        if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
-        print(json.dumps(line), flush=True)
+    if gather is not None:
+        wd = Watchdog(args.gather_timeout, emit_line)
+        try:
+            if mode == "torchrun":
+                uid = [capi.comm_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                group = capi.Group(buffer_size=n, rank=rank, nranks=world, unique_id=uid[0], precision=args.precision,
+                                   device=d0)
+            else:
+                group = capi.Group(buffer_size=n, devices=devs.devs, precision=args.precision)
+            comm = group.comm_info()
+            gather["rccl_comm"] = {"ranks": comm[0], "rank": comm[1], "device": comm[2], "group_ranks": group.nranks,
+                                   "local_ranks": group.num_local}
+            if group.nranks != gpus or comm[0] != gpus or comm[2] != d0 or comm[1] != group.first_local:
+                raise RuntimeError("the RCCL communicator reports %s for a %d-GPU job on device %d" % (comm, gpus, d0))
+            # rank 0 holds the whole job's feature record; the other ranks only their transfer
+            # buffers (two output sets: consecutive steps are in flight together, pipelined())
+            root = group.first_local == 0
+            with torch.cuda.device(d0):
+                sets = [plan.alloc_outputs(F * gpus if root else 1, FEATURES, device="cuda:%d" % d0) for _ in range(2)]
+            mask = capi.output_mask(sets[0][1])
+            ptrs = [frames[d].data_ptr() for d in devs.devs]
+
+            def step_gather(k):
+                group.extract_device(ptrs, [F] * gpus, sets[k & 1][1] if root else None, mask, args.chunks,
+                                     [devs.stream(d, k).cuda_stream for d in devs.devs])
+            settle(step_gather, devs, args.settle_ms, dist)
+            el_g, km_g, stats_g = run_mode(step_gather, devs, args.steps, args.warmup, dist)
+            if root:  # spot check: the gathered record holds every rank's shard (last frame of each)
+                chk = sets[0][0]["zcr"].view(gpus, F)[:, -1]
+                gather["finite_last_frames"] = bool(torch.all((chk >= 0) & (chk < n)).item())
+            gather.update({"status": "ok", "value": gpus * F * args.steps / el_g, "ms_per_step": el_g / args.steps * 1e3,
+                           "kernel_ms": km_g, "step_event_ms": stats_g})
+            wd.cancel()
+        except Exception as e:  # the line still reports the shards, with the gather's failure
+            print("rank %d: gather failed: %r" % (rank, e), file=sys.stderr, flush=True)
+            gather["status"] = "failed on rank %d: %r" % (rank, e)
+            if rank == 0:
+                emit_line()
+                os._exit(0)
+            wd.t.join()  # a failed peer waits for its deadline (rank 0 may be blocked on it)
+    extras = {}
+    if mode == "one":
+        extras = secondary(args, plan, frames[d0], devs, n, F)
+    line_box.update(extras)
+    emit_line()
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def secondary(args, plan, frames, devs, n, F):
+    """Single-GPU secondary fields (never `value`): fast precision, config C4 exactly, every
+    output, the live PMC counters, the PCIe-inclusive host path and the CPU baseline."""
+    out = {}
+    dev = devs.devs[0]
+
+    def timed(p, feats, bytes_per_frame):
+        sets = [p.alloc_outputs(F, feats) for _ in range(2)]
+
+        def st(k):
+            p.extract_device(frames.data_ptr(), F, sets[k & 1][1], devs.stream(dev, k).cuda_stream)
+        settle(st, devs, args.settle_ms)
+        el, km, stats = run_mode(st, devs, args.steps, args.warmup, None)
+        return {"value": F * args.steps / el, "unit": "frames/s", "kernel_ms": km,
+                "kernel_ms_launch_alone": stats["launch_alone_median_ms"], "bytes_per_frame": bytes_per_frame,
+                "roofline_frac": F * bytes_per_frame / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    if not args.no_fast and args.precision != "fast":
+        # BASELINE.md: the fp32-butterfly mode beside the faithful one (same features and frames)
+        out["fast_mode"] = dict(timed(capi.Plan(buffer_size=n, precision="fast", device=dev), FEATURES,
+                                      4 * n + 4 * OUT_FLOATS), precision="fast (f32 butterflies; not bit-faithful)")
+    if not args.no_c4:
+        # BASELINE config C4 exactly: 40-band mel + 13 MFCC, nothing else (SURVEY §8(d): 4,148 B/frame)
+        out["c4"] = dict(timed(capi.Plan(buffer_size=n, precision=args.precision, num_mel_bands=40, device=dev),
+                               ["mfcc"], 4 * n + 4 * 13), features=["mfcc"], mel_bands=40, mfcc_coeffs=13)
+    if not args.no_c3:
+        # BASELINE config C3: spectral* + loudness + perceptual (SURVEY §8(d): 4,232 B/frame)
+        feats3 = [f for f in FEATURES if f not in ("rms", "energy", "zcr", "mfcc")]
+        out["c3"] = dict(timed(plan, feats3, 4 * n + 4 * (7 + 25 + 2)), features=feats3)
+    if not args.no_every_output:
+        # EVERY output of the path -- the headline set plus the amplitude, power and complex
+        # spectra -- with the 40-band mel of config C4, same frames
+        feats_e = FEATURES + ["amplitudeSpectrum", "powerSpectrum", "complexSpectrum"]
+        out["every_output"] = dict(timed(capi.Plan(buffer_size=n, precision=args.precision, num_mel_bands=40, device=dev),
+                                         feats_e, 4 * n + 4 * (OUT_FLOATS + 2 * (n // 2) + 2 * n)),
+                                   features=feats_e, mel_bands=40)
+    if not args.no_pmc:
+        try:
+            out["pmc"] = pmc_live(n, F, args.precision)
+        except Exception as e:  # the counters are a report, never the measurement itself
+            out["pmc"] = (None, None, "rocprofv3 passes failed: %r" % (e,))
+    if not args.no_host_path:
+        out["host_path"] = host_path(plan, frames)
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+    return out
+
+
+def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, gather, extras):
+    bytes_per_frame = 4 * n + 4 * OUT_FLOATS
+    use_gather = gather is not None and gather.get("status") == "ok"
+    value = gather["value"] if use_gather else value_s
+    elapsed = args.steps * 1e3 / (value / (gpus * F))  # ms for the K steps
+    kernel_ms = km_s  # the shards' launch period: the roofline of the extraction kernel
+    alone_ms = (stats_s["rank0"] if "rank0" in stats_s else stats_s)["launch_alone_median_ms"]
+    achieved = F * bytes_per_frame / (kernel_ms * 1e-3) / 1e9
+    traffic, valu, traffic_note = extras.get("pmc") or (None, None, "not measured (--no-pmc or N > 1)")
+    if valu is not None:
+        # SURVEY §8(d): the faithful path is FP64-VALU bound. Issue costs per wave64
+        # instruction measured by tools/ubench/op_rates.hip (profiles/r01_op_rates.log):
+        # f64 ~5.0, f32<->f64 conversion 4.2 cycles; at the clock this run's kernel time implies
+        cyc = kernel_ms * 1e-3 * 2.4e9 * 1024 / F  # SIMD cycles per frame (2.4 GHz held, 1,024 SIMDs)
+        valu["frame_simd_cycles"] = cyc
+        valu["est_fp64_cvt_busy"] = (valu["f64_per_frame"] * 5.0 + valu["cvt_per_frame"] * 4.2) / cyc
+        # FP64 pipe (vector and matrix share it): 78.6 TFLOP/s dense on MI355X (1,024 SIMDs x 32
+        # FLOP/clk x 2.4 GHz; v_mfma_f64_4x4x4 issues every 16 cycles: tools/ubench/op_rates.hip)
+        mf = valu["mfma_f64"]
+        mf["tflops"] = mf["flop_per_launch"] / (kernel_ms * 1e-3) / 1e12
+        mf["peak_tflops"] = 78.6
+        mf["frac"] = mf["tflops"] / mf["peak_tflops"]
+    line = {
+        "metric": "audio frames/sec (bufferSize=1024, all features) at 1/2/4/8 GPUs; % HBM roofline",
+        "value": value,
+        "unit": "frames/s",
+        "n_gpus": gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64 butterflies / f32 storage" if args.precision == "faithful" else "f32",
+        "data": "synthetic (seeded splitmix64 PCM generated in HBM)",
+        "config": {"workload": "C3+C4 feature set: %d frames x bufferSize=%d per GPU; 13 scalars (rms, energy, zcr, "
+                               "7 spectral*, loudness.total, perceptualSpread, perceptualSharpness) + "
+                               "loudness.specific[24] + mfcc[13] of 26 mel bands, float32 outputs; no spectra" % (F, n),
+                   "buffer_size": n, "frames_per_gpu": F, "features": FEATURES,
+                   "mel_bands": 26, "mfcc_coeffs": 13, "precision": args.precision,
+                   "parallelism": {"torchrun": "frame shards, one process per GPU (%d)" % gpus,
+                                   "single": "frame shards, one process driving %d GPUs" % gpus,
+                                   "one": "one GPU"}[mode],
+                   "devices": placement,
+                   "gather_to_rank0": use_gather,
+                   "value_source": ("steps with the RCCL gather of every rank's records to rank 0 inside the timed "
+                                    "step" if use_gather else "the shards, no gather")},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
+                     "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
+                     "kernel_ms_source": "launch period: HIP events around the timed region / steps "
+                                         "(steps pipelined over two streams); a launch on its own: step_event_ms",
+                     "frac_launch_alone": F * bytes_per_frame / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "step_event_ms": stats_s,
+                     "bytes_per_frame": bytes_per_frame},
+    }
+    if gpus > 1:
+        line["shards_only"] = {"value": value_s, "ms_per_step": el_s / args.steps * 1e3,
+                               "note": "every rank's shard extracted, no gather"}
+        line["gather"] = gather if gather is not None else {"status": "off (--no-gather or shared GPUs)"}
+    if valu:
+        line["valu"] = valu
+    for k in ("fast_mode", "c3", "c4", "every_output", "host_path", "cpu_baseline"):
+        if k in extras:
+            line[k] = extras[k]
+    return line
 
 
 if __name__ == "__main__":

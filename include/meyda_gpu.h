@@ -270,10 +270,20 @@ int mgx_group_create_rank(const mgx_plan_desc* desc, const void* unique_id, uint
  * else -- shards, chunks, transfer slots, the two compute streams, the root's unpack -- is
  * the multi-device path's own code, so one GPU can check the gather byte for byte. */
 int mgx_group_create_loopback(const mgx_plan_desc* desc, uint32_t nranks, mgx_group** out);
+/* The same test group with the RCCL transport: the root holds a one-rank RCCL
+ * communicator on desc->device, and each peer chunk crosses as an ncclSend to self matched
+ * by an ncclRecv from self (one ncclGroupStart/End each) on the root's communication
+ * stream -- the RCCL calls, message sizes, slot ordering and unpack of the multi-rank
+ * path, runnable on one GPU (RCCL refuses two ranks on one device). */
+int mgx_group_create_loopback_rccl(const mgx_plan_desc* desc, uint32_t nranks, mgx_group** out);
 int mgx_group_destroy(mgx_group* group);
 /* Ranks of the group, and the ranks this process drives (num_local = 1 per process, or
  * all of them in single-process mode, first_local = their first rank). */
 int mgx_group_info(const mgx_group* group, uint32_t* nranks, uint32_t* first_local, uint32_t* num_local);
+/* What the RCCL communicator of this process's first local rank reports: ranks in the
+ * communicator (ncclCommCount), this rank in it (ncclCommUserRank) and its device
+ * (ncclCommCuDevice); all -1 when the group has no communicator (one rank, or device copies). */
+int mgx_group_comm_info(const mgx_group* group, int32_t* comm_ranks, int32_t* comm_rank, int32_t* comm_device);
 
 /* Device-resident batch. frames[i]: device pointer of the shard of local rank
  * first_local + i (on that rank's device); counts: frames of every rank (nranks

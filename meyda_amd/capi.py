@@ -35,8 +35,8 @@ EXPORTS = ["mgx_plan_desc_init", "mgx_plan_create", "mgx_plan_destroy", "mgx_pla
            "mgx_feature_info", "mgx_device_count", "mgx_abi_version", "mgx_last_error",
            "mgx_wav_parse", "mgx_pcm_decode_device", "mgx_extract_host_pcm",
            "mgx_shard_range", "mgx_packed_layout", "mgx_comm_unique_id", "mgx_group_create",
-           "mgx_group_create_rank", "mgx_group_create_loopback", "mgx_group_destroy", "mgx_group_info", "mgx_group_extract_device",
-           "mgx_group_extract_host"]
+           "mgx_group_create_rank", "mgx_group_create_loopback", "mgx_group_create_loopback_rccl", "mgx_group_destroy",
+           "mgx_group_info", "mgx_group_comm_info", "mgx_group_extract_device", "mgx_group_extract_host"]
 COMM_ID_BYTES = 128
 FLAG_DCT_SEQUENTIAL = 1  # mgx_plan_desc.flags
 FLAG_MFCC_REFERENCE = 2  # mel sums, log and DCT in the reference's own order
@@ -143,7 +143,11 @@ def lib():
                                             ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
         L.mgx_group_create_loopback.argtypes = [ctypes.POINTER(PlanDesc), ctypes.c_uint32,
                                                 ctypes.POINTER(ctypes.c_void_p)]
+        L.mgx_group_create_loopback_rccl.argtypes = [ctypes.POINTER(PlanDesc), ctypes.c_uint32,
+                                                     ctypes.POINTER(ctypes.c_void_p)]
         L.mgx_group_destroy.argtypes = [ctypes.c_void_p]
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        L.mgx_group_comm_info.argtypes = [ctypes.c_void_p, i32p, i32p, i32p]
         L.mgx_group_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
                                      ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
         L.mgx_group_extract_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), u64p,
@@ -374,14 +378,19 @@ class Group:
 
     Group(devices=[0, 1, ...], **plan_kw)                 one process, several devices
     Group(rank=r, nranks=n, unique_id=b, device=d, ...)   one process per device (torchrun)
-    Group(loopback=n, device=d, ...)                      test transport: n ranks on one device
+    Group(loopback=n, device=d, ...)                      test transport: n ranks on one device,
+                                                          chunks as device copies
+    Group(loopback=n, transport="rccl", device=d, ...)    the same, chunks as RCCL send/recv to
+                                                          self on a one-rank communicator
     """
 
-    def __init__(self, buffer_size=512, devices=None, rank=None, nranks=None, unique_id=None, loopback=None, **kw):
+    def __init__(self, buffer_size=512, devices=None, rank=None, nranks=None, unique_id=None, loopback=None,
+                 transport="copy", **kw):
         h = ctypes.c_void_p()
         if loopback is not None:
             self.desc = make_desc(buffer_size=buffer_size, **kw)
-            check(lib().mgx_group_create_loopback(ctypes.byref(self.desc), loopback, ctypes.byref(h)))
+            create = {"copy": lib().mgx_group_create_loopback, "rccl": lib().mgx_group_create_loopback_rccl}[transport]
+            check(create(ctypes.byref(self.desc), loopback, ctypes.byref(h)))
         elif devices is not None:
             self.desc = make_desc(buffer_size=buffer_size, device=devices[0], **kw)
             arr = (ctypes.c_int32 * len(devices))(*devices)
@@ -395,6 +404,13 @@ class Group:
         nr, first, nl = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
         check(lib().mgx_group_info(h, ctypes.byref(nr), ctypes.byref(first), ctypes.byref(nl)))
         self.nranks, self.first_local, self.num_local = nr.value, first.value, nl.value
+
+    def comm_info(self):
+        """(ranks, rank, device) as this process's RCCL communicator reports them, or
+        (-1, -1, -1) without one (mgx_group_comm_info)."""
+        n, r, d = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(lib().mgx_group_comm_info(self._h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d)))
+        return n.value, r.value, d.value
 
     def close(self):
         if getattr(self, "_h", None):

@@ -40,6 +40,10 @@ struct Rccl {
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
+  // what the communicator itself reports (mgx_group_comm_info)
+  ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*CommUserRank)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*CommCuDevice)(const ncclComm_t, int*) = nullptr;
 };
 
 // Loaded once per process: $MGX_RCCL_LIB, else librccl.so.1 from the loader path, else
@@ -69,6 +73,9 @@ Rccl* rccl() {
   sym(r.Send, "ncclSend");
   sym(r.Recv, "ncclRecv");
   sym(r.GetErrorString, "ncclGetErrorString");
+  sym(r.CommCount, "ncclCommCount");
+  sym(r.CommUserRank, "ncclCommUserRank");
+  sym(r.CommCuDevice, "ncclCommCuDevice");
   r.ok = all;
   return r.ok ? &r : nullptr;
 }
@@ -223,12 +230,21 @@ int ensure(unsigned char** p, uint64_t* cap, uint64_t bytes, const char* what) {
 
 }  // namespace
 
+// How a peer's chunk reaches the root's staging slot.
+enum class Transport {
+  kRccl,      // ncclSend on the peer's communication stream, ncclRecv on the root's
+  kCopy,      // mgx_group_create_loopback: a device copy on the root's communication stream
+  kRcclSelf,  // mgx_group_create_loopback_rccl: ncclSend + ncclRecv to self on a one-rank
+              // communicator, on the root's communication stream
+};
+
 struct mgx_group {
   mgx_plan_desc d;
   uint32_t nranks = 0;
   bool single_process = true;
-  bool loopback = false;  // mgx_group_create_loopback: one device, transfers as device copies
+  Transport transport = Transport::kRccl;
   std::vector<Member> m;  // local ranks, in rank order
+  bool loopback() const { return transport != Transport::kRccl; }  // all ranks on one device
 };
 
 extern "C" {
@@ -295,7 +311,7 @@ int mgx_group_create(const mgx_plan_desc* desc, const int32_t* devices, uint32_t
   return MGX_OK;
 }
 
-int mgx_group_create_loopback(const mgx_plan_desc* desc, uint32_t nranks, mgx_group** out) {
+static int create_loopback(const mgx_plan_desc* desc, uint32_t nranks, Transport tr, mgx_group** out) {
   if (!out) return fail(MGX_E_INVALID_ARGUMENT, "out is NULL");
   *out = nullptr;
   if (!desc || nranks == 0) return fail(MGX_E_INVALID_ARGUMENT, "a descriptor and at least one rank are required");
@@ -303,7 +319,7 @@ int mgx_group_create_loopback(const mgx_plan_desc* desc, uint32_t nranks, mgx_gr
   g->d = *desc;
   g->nranks = nranks;
   g->single_process = true;
-  g->loopback = true;
+  g->transport = tr;
   g->m.resize(nranks);
   int rc = MGX_OK;
   for (uint32_t i = 0; i < nranks && !rc; ++i) {
@@ -311,12 +327,33 @@ int mgx_group_create_loopback(const mgx_plan_desc* desc, uint32_t nranks, mgx_gr
     g->m[i].device = desc->device;
     rc = member_init(g->m[i], *desc);
   }
+  if (!rc && tr == Transport::kRcclSelf) {
+    // one communicator of one rank on the device, held by the root: every peer's chunk is a
+    // send to self matched by a receive from self
+    Rccl* r = rccl();
+    if (!r) {
+      rc = fail(MGX_E_UNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
+    } else {
+      const int dev = desc->device;
+      (void)hipSetDevice(dev);
+      ncclResult_t e = r->CommInitAll(&g->m[0].comm, 1, &dev);
+      if (e != ncclSuccess) rc = rccl_fail(e, "ncclCommInitAll (one rank)");
+    }
+  }
   if (rc) {
     mgx_group_destroy(g);
     return rc;
   }
   *out = g;
   return MGX_OK;
+}
+
+int mgx_group_create_loopback(const mgx_plan_desc* desc, uint32_t nranks, mgx_group** out) {
+  return create_loopback(desc, nranks, Transport::kCopy, out);
+}
+
+int mgx_group_create_loopback_rccl(const mgx_plan_desc* desc, uint32_t nranks, mgx_group** out) {
+  return create_loopback(desc, nranks, Transport::kRcclSelf, out);
 }
 
 int mgx_group_create_rank(const mgx_plan_desc* desc, const void* unique_id, uint32_t nranks, uint32_t rank,
@@ -368,9 +405,53 @@ int mgx_group_info(const mgx_group* g, uint32_t* nranks, uint32_t* first_local, 
   return MGX_OK;
 }
 
+int mgx_group_comm_info(const mgx_group* g, int32_t* comm_ranks, int32_t* comm_rank, int32_t* comm_device) {
+  if (!g) return fail(MGX_E_INVALID_ARGUMENT, "group is NULL");
+  int32_t n = -1, me = -1, dev = -1;
+  const ncclComm_t c = g->m.empty() ? nullptr : g->m[0].comm;
+  if (c) {
+    Rccl* r = rccl();
+    int v;
+    if (!r) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
+    if (r->CommCount(c, &v) != ncclSuccess) return fail(MGX_E_DEVICE, "ncclCommCount failed");
+    n = v;
+    if (r->CommUserRank(c, &v) != ncclSuccess) return fail(MGX_E_DEVICE, "ncclCommUserRank failed");
+    me = v;
+    if (r->CommCuDevice(c, &v) != ncclSuccess) return fail(MGX_E_DEVICE, "ncclCommCuDevice failed");
+    dev = v;
+  }
+  if (comm_ranks) *comm_ranks = n;
+  if (comm_rank) *comm_rank = me;
+  if (comm_device) *comm_device = dev;
+  return MGX_OK;
+}
+
+static int group_extract(mgx_group* g, const float* const* frames, const uint64_t* counts, const mgx_outputs* root_out,
+                         uint32_t mask, uint32_t nch, void* const* streams, std::vector<hipStream_t>& cs);
+
 int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uint64_t* counts,
                              const mgx_outputs* root_out, uint32_t mask, uint32_t nch, void* const* streams) {
   if (!g || !frames || !counts) return fail(MGX_E_INVALID_ARGUMENT, "NULL argument");
+  std::vector<hipStream_t> cs;
+  const int rc = group_extract(g, frames, counts, root_out, mask, nch, streams, cs);
+  if (rc && !cs.empty()) {
+    // An error after work was enqueued: chunks may still be in flight on the second compute
+    // stream and the communication stream (writing the root's outputs or reading transfer
+    // slots). Join them into the callers' streams, so what a caller enqueues next stays
+    // ordered after them, without a host wait (a peer that never posts its half of a message
+    // would make a synchronisation hang).
+    for (size_t i = 0; i < g->m.size() && i < cs.size(); ++i) {
+      Member& m = g->m[i];
+      (void)hipSetDevice(m.device);
+      if (hipEventRecord(m.ev_comp_done, m.s_alt) == hipSuccess) (void)hipStreamWaitEvent(cs[i], m.ev_comp_done, 0);
+      if (hipEventRecord(m.ev_comm_done, m.s_comm) == hipSuccess) (void)hipStreamWaitEvent(cs[i], m.ev_comm_done, 0);
+    }
+  }
+  return rc;
+}
+
+static int group_extract(mgx_group* g, const float* const* frames, const uint64_t* counts, const mgx_outputs* root_out,
+                         uint32_t mask, uint32_t nch, void* const* streams, std::vector<hipStream_t>& cs) {
   if (mask & ~MGX_OUT_ALL_MASK) return fail(MGX_E_INVALID_ARGUMENT, "unknown output bits in mask 0x%x", mask);
   const mgx_plan_desc& d = g->d;
   const uint32_t R = g->nranks;
@@ -423,18 +504,29 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
   // it drains instead of starting after its last workgroup. 8 chunks of 262,144 x 1024 on one
   // stream took 9 % longer than one launch; alternating, 1 % less. Chunk c and
   // c+2 share a transfer slot and a stream, so the slot's reuse stays ordered on that stream.
-  std::vector<hipStream_t> cs(g->m.size());
+  for (size_t i = 0; i < g->m.size(); ++i) cs.push_back(streams ? static_cast<hipStream_t>(streams[i]) : g->m[i].s_comp);
   for (size_t i = 0; i < g->m.size(); ++i) {
     Member& m = g->m[i];
-    cs[i] = streams ? static_cast<hipStream_t>(streams[i]) : m.s_comp;
     if (R == 1 && nch == 1) continue;
     HIP_OK(hipSetDevice(m.device), "hipSetDevice");
     HIP_OK(hipEventRecord(m.ev_start, cs[i]), "hipEventRecord");
     if (nch > 1) HIP_OK(hipStreamWaitEvent(m.s_alt, m.ev_start, 0), "hipStreamWaitEvent");
     if (R > 1) HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_start, 0), "hipStreamWaitEvent");
   }
-  Rccl* rc_ = R > 1 && !g->loopback ? rccl() : nullptr;
-  if (R > 1 && !g->loopback && !rc_) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
+  const bool uses_rccl = R > 1 && g->transport != Transport::kCopy;
+  Rccl* rc_ = uses_rccl ? rccl() : nullptr;
+  if (uses_rccl && !rc_) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
+  // one RCCL group of point-to-point calls; on an error after ncclGroupStart the group is
+  // still ended (an open group would absorb the caller's next RCCL calls)
+  auto p2p_group = [&](auto&& body) -> int {
+    NCCL_OK(rc_->GroupStart(), "ncclGroupStart");
+    const char* what = nullptr;
+    const ncclResult_t e = body(what);
+    const ncclResult_t e_end = rc_->GroupEnd();
+    if (e != ncclSuccess) return rccl_fail(e, what);
+    if (e_end != ncclSuccess) return rccl_fail(e_end, "ncclGroupEnd");
+    return MGX_OK;
+  };
   for (uint32_t c = 0; c < nch; ++c) {
     const int sl = (int)(c & 1);
     // extraction of chunk c on every local rank
@@ -463,9 +555,10 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
       }
     }
     if (R == 1) continue;
-    if (g->loopback) {
-      // the test transport: each peer's chunk copied into the root's staging slot on the
-      // root's communication stream, after the peer's extraction of it
+    if (g->loopback()) {
+      // the test transports: each peer's chunk into the root's staging slot on the root's
+      // communication stream, after the peer's extraction of it -- a device copy, or an RCCL
+      // send to self matched by a receive from self on the root's one-rank communicator
       Member& root = g->m[0];
       HIP_OK(hipSetDevice(root.device), "hipSetDevice");
       for (uint32_t p = 1; p < R; ++p) {
@@ -473,37 +566,56 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
         uint64_t c0, cn;
         chunk_of(counts[p], nch, c, &c0, &cn);
         HIP_OK(hipStreamWaitEvent(root.s_comm, m.ev_comp[sl], 0), "hipStreamWaitEvent");
-        if (cn)
-          HIP_OK(hipMemcpyAsync(root.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot, m.xfer + sl * slot,
-                                packed_layout(d, mask, cn, nullptr), hipMemcpyDeviceToDevice, root.s_comm),
+        unsigned char* dst = root.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot;
+        const uint64_t bytes = packed_layout(d, mask, cn, nullptr);
+        if (cn && g->transport == Transport::kCopy) {
+          HIP_OK(hipMemcpyAsync(dst, m.xfer + sl * slot, bytes, hipMemcpyDeviceToDevice, root.s_comm),
                  "hipMemcpyAsync(loopback chunk)");
+        } else if (cn) {
+          const int rc = p2p_group([&](const char*& what) {
+            what = "ncclSend (self)";
+            ncclResult_t e = rc_->Send(m.xfer + sl * slot, bytes, ncclUint8, 0, root.comm, root.s_comm);
+            if (e != ncclSuccess) return e;
+            what = "ncclRecv (self)";
+            return rc_->Recv(dst, bytes, ncclUint8, 0, root.comm, root.s_comm);
+          });
+          if (rc) return rc;
+        }
         HIP_OK(hipEventRecord(m.ev_sent[sl], root.s_comm), "hipEventRecord");
         m.xfer_sent[sl] = true;
       }
     } else {
-    // transfers of chunk c (one group: in single-process mode it spans every device)
-    NCCL_OK(rc_->GroupStart(), "ncclGroupStart");
-    for (Member& m : g->m) {
-      if (m.rank == 0) {
-        for (uint32_t p = 1; p < R; ++p) {
-          uint64_t c0, cn;
-          chunk_of(counts[p], nch, c, &c0, &cn);
-          if (!cn) continue;
-          unsigned char* st = m.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot;
-          NCCL_OK(rc_->Recv(st, packed_layout(d, mask, cn, nullptr), ncclUint8, (int)p, m.comm, m.s_comm), "ncclRecv");
+      // transfers of chunk c (one group: in single-process mode it spans every device)
+      const int rc = p2p_group([&](const char*& what) {
+        for (Member& m : g->m) {
+          if (m.rank == 0) {
+            for (uint32_t p = 1; p < R; ++p) {
+              uint64_t c0, cn;
+              chunk_of(counts[p], nch, c, &c0, &cn);
+              if (!cn) continue;
+              unsigned char* st = m.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot;
+              what = "ncclRecv";
+              const ncclResult_t e = rc_->Recv(st, packed_layout(d, mask, cn, nullptr), ncclUint8, (int)p, m.comm, m.s_comm);
+              if (e != ncclSuccess) return e;
+            }
+          } else {
+            uint64_t c0, cn;
+            chunk_of(counts[m.rank], nch, c, &c0, &cn);
+            what = "ncclSend";
+            const ncclResult_t e =
+                cn ? rc_->Send(m.xfer + sl * slot, packed_layout(d, mask, cn, nullptr), ncclUint8, 0, m.comm, m.s_comm)
+                   : ncclSuccess;
+            if (e != ncclSuccess) return e;
+          }
         }
-      } else {
-        uint64_t c0, cn;
-        chunk_of(counts[m.rank], nch, c, &c0, &cn);
-        if (cn) NCCL_OK(rc_->Send(m.xfer + sl * slot, packed_layout(d, mask, cn, nullptr), ncclUint8, 0, m.comm, m.s_comm), "ncclSend");
-      }
-    }
-    NCCL_OK(rc_->GroupEnd(), "ncclGroupEnd");
+        return ncclSuccess;
+      });
+      if (rc) return rc;
     }
     for (Member& m : g->m) {
       HIP_OK(hipSetDevice(m.device), "hipSetDevice");
       if (m.rank != 0) {
-        if (!g->loopback) {
+        if (!g->loopback()) {
           HIP_OK(hipEventRecord(m.ev_sent[sl], m.s_comm), "hipEventRecord");
           m.xfer_sent[sl] = true;
         }
@@ -539,7 +651,7 @@ int mgx_group_extract_device(mgx_group* g, const float* const* frames, const uin
       HIP_OK(hipEventRecord(m.ev_comp_done, m.s_alt), "hipEventRecord");
       HIP_OK(hipStreamWaitEvent(cs[i], m.ev_comp_done, 0), "hipStreamWaitEvent");
     }
-    if (R > 1 && g->loopback && m.rank != 0) {  // its chunks leave on the root's stream
+    if (R > 1 && g->loopback() && m.rank != 0) {  // its chunks leave on the root's stream
       for (uint32_t sl = 0; sl < std::min<uint32_t>(nch, 2); ++sl)
         HIP_OK(hipStreamWaitEvent(cs[i], m.ev_sent[sl], 0), "hipStreamWaitEvent");
     } else if (R > 1) {

@@ -1604,20 +1604,6 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   return sc == MGX_RMS ? sqrt_d(v) : sc == MGX_PERCEPTUAL_SPREAD ? v * v : v;
 }
 
-// Work shares of the four workgroup ranks of a CU at N = 1024 (sum 64; extract_kernel).
-#ifndef MGX_RANK_SHARES
-#define MGX_RANK_SHARES 1  // the other N: linear rank weights A (R - 1) - r
-#endif
-#ifndef MGX_RANK_A
-#define MGX_RANK_A 2  // A = 2: 2:1 from the first rank to the last; 3: 1.5:1
-#endif
-#ifndef MGX_SHARE0
-#define MGX_SHARE0 22
-#define MGX_SHARE1 17
-#define MGX_SHARE2 14
-#define MGX_SHARE3 11
-#endif
-
 // Copy of the TwLds image from the plan tables, once per workgroup (before its LDS barrier).
 template <int N, int P, int I>
 __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
@@ -1707,27 +1693,42 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // blockIdx order (rank r = blockIdx / (grid / 4) on every CU), and at equal priority the
   // SIMD's arbiter favours the oldest wave, so with equal shares rank 0 finished at 64 % of
   // the launch and the SIMDs ran 3, 2, then 1 wave for the rest (tools/wave_times.py).
-  // Rank r takes MGX_SHARE_r / 64 of the groups instead.
+  // Rank r takes a share of its own instead (22 / 18 / 14 / 10 of 64 at N = 1024).
   const uint64_t ng = (nb + 3) / 4;
   uint64_t g0, g1;
   const uint64_t nr = (uint64_t)ap->wg_ranks;
   // (unequal shares need many groups per workgroup: with a few each, their rounding unbalances
   // more than the ranks' rates do -- C2's 65,536 frames at N = 512 lost 6 %; and N = 256 lost 4 %)
   const bool many = ng >= 8 * (uint64_t)gridDim.x;
-  if (N >= 512 && N != 1024 && MGX_RANK_SHARES && many && nr >= 2 && nr <= 8 && gridDim.x % nr == 0) {
+  // Every boundary between two workgroups' ranges falls on an even group (32 frames): the
+  // 4-byte scalar outputs of a workgroup then fill whole 128-byte lines (and the 52-byte MFCC
+  // and 96-byte loudness records whole lines too), so no output line is written from two
+  // XCDs' L2s. Shares ending on odd groups took WRITE_SIZE to 1.8x the outputs (12x for the
+  // time-only set); ev() rounds a boundary down to even, the last range ends at ng.
+  auto ev = [](uint64_t g) { return g & ~(uint64_t)1; };
+  // [lo, hi) over q workgroups in pairs of groups, the remainder pairs one each to the first
+  // workgroups (balanced to one pair; the last pair may be a single group at ng)
+  auto split = [&](uint64_t lo, uint64_t hi, uint64_t q, uint64_t i) {
+    const uint64_t np = (hi - lo + 1) / 2, base = np / q, rem = np % q;
+    const uint64_t a = lo + 2 * (i * base + (i < rem ? i : rem)), b = a + 2 * (base + (i < rem ? 1 : 0));
+    g0 = a < hi ? a : hi;
+    g1 = b < hi ? b : hi;
+  };
+  if (N >= 512 && N != 1024 && many && nr >= 2 && nr <= 8 && gridDim.x % nr == 0) {
     // other N: rank r's weight 2 (R - 1) - r, from 2:1 for the first rank to the last
     const uint64_t q = gridDim.x / nr, r = blockIdx.x / q, i = blockIdx.x % q;
-    auto cum = [&](uint64_t k) { return k * MGX_RANK_A * (nr - 1) - k * (k - 1) / 2; };
-    const uint64_t cs = cum(nr), lo = ng * cum(r) / cs, hi = ng * cum(r + 1) / cs, per = (hi - lo + q - 1) / q;
-    g0 = lo + i * per < hi ? lo + i * per : hi;
-    g1 = g0 + per < hi ? g0 + per : hi;
+    auto cum = [&](uint64_t k) { return k * 2 * (nr - 1) - k * (k - 1) / 2; };
+    const uint64_t cs = cum(nr);
+    split(ev(ng * cum(r) / cs), r + 1 == nr ? ng : ev(ng * cum(r + 1) / cs), q, i);
   } else if (N == 1024 && many && nr == 4 && (gridDim.x & 3) == 0) {
-    constexpr uint64_t c1 = MGX_SHARE0, c2 = c1 + MGX_SHARE1, c3 = c2 + MGX_SHARE2, cs = c3 + MGX_SHARE3;
+    // shares 22 / 18 / 14 / 10 of 64 for ranks 0..3 (linear, 2.2:1; 22 / 17 / 14 / 11 before
+    // the pair granularity: a 262,144-frame batch's 17 / 64 is 8.5 pairs per workgroup)
+    constexpr uint64_t c1 = 22, c2 = c1 + 18, c3 = c2 + 14, cs = c3 + 10;
     const uint64_t q = gridDim.x / 4, r = blockIdx.x / q, i = blockIdx.x % q;
     const uint64_t ca = r == 0 ? 0 : r == 1 ? c1 : r == 2 ? c2 : c3, cb = r == 0 ? c1 : r == 1 ? c2 : r == 2 ? c3 : cs;
-    const uint64_t lo = ng * ca / cs, hi = ng * cb / cs, per = (hi - lo + q - 1) / q;
-    g0 = lo + i * per < hi ? lo + i * per : hi;
-    g1 = g0 + per < hi ? g0 + per : hi;
+    split(ev(ng * ca / cs), r == 3 ? ng : ev(ng * cb / cs), q, i);
+  } else if (many) {
+    split(0, ng, gridDim.x, blockIdx.x);
   } else {
     const uint64_t per = (ng + gridDim.x - 1) / gridDim.x;
     g0 = (uint64_t)blockIdx.x * per;

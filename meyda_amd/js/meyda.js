@@ -18,6 +18,8 @@
 //   flush()                         deliver buffered callbacks now (options.batchFrames > 1)
 //   options.devices = [0, 1, ...]   shard batches over several GPUs; the feature records are
 //                                   gathered to the first one by RCCL (one plan per device)
+//   options.asyncPlans = 2          plans per window that async batch jobs run on; more jobs
+//                                   queue on them
 //
 // Streaming (start/stop, src/meyda.js:69-91,233-241): with options.batchFrames = K > 1
 // the buffers pushed by process() are queued and extracted K at a time in one launch;
@@ -124,15 +126,26 @@ class Meyda {
   }
 
   // Async batch jobs own their plan for the whole job (the addon marks it busy), so they
-  // never run on the streaming plan: per window, a pool grown on demand, so onaudioprocess
-  // buffers and further async batches proceed while a job is in flight.
-  _asyncPlan() {
+  // never run on the streaming plan: per window, a pool of at most options.asyncPlans plans
+  // (default 2; with options.devices each one is a whole device group with its RCCL
+  // communicators), so onaudioprocess buffers and a second async batch proceed while a job
+  // is in flight. Further jobs queue on the pooled plan with the fewest pending jobs.
+  _runAsync(job) {
     const w = this._window();
     const pool = this._asyncPlans[w] || (this._asyncPlans[w] = []);
-    for (const p of pool) if (!addon.planBusy(p)) return p;
-    const p = this._newPlan(w);
-    pool.push(p);
-    return p;
+    const cap = Math.max(1, this.options.asyncPlans | 0 || 2);
+    let slot = pool.find((sl) => sl.pending === 0);
+    if (!slot && pool.length < cap) {
+      slot = { plan: this._newPlan(w), pending: 0, tail: Promise.resolve() };
+      pool.push(slot);
+    }
+    if (!slot) slot = pool.reduce((a, b) => (b.pending < a.pending ? b : a));
+    slot.pending++;
+    const run = () => job(slot.plan);
+    const res = slot.tail.then(run, run);
+    const done = () => { slot.pending--; };
+    slot.tail = res.then(done, done);
+    return res;
   }
 
   // The per-buffer handler (src/meyda.js:69-91): take the buffer, then deliver the
@@ -265,7 +278,8 @@ class Meyda {
 
   getBatchAsync(features, frames) {
     const names = checkBatchNames(features);
-    return addon.extractAsync(this._asyncPlan(), toF32(frames), names);
+    const x = toF32(frames);
+    return this._runAsync((plan) => addon.extractAsync(plan, x, names));
   }
 
   // Every full buffer of a .wav file (Buffer / Uint8Array / ArrayBuffer), channel `channel`.
@@ -274,7 +288,8 @@ class Meyda {
   }
 
   getBatchWavAsync(features, wavBytes, channel) {
-    return addon.extractWavAsync(this._asyncPlan(), wavBytes, checkBatchNames(features), channel | 0);
+    const names = checkBatchNames(features);
+    return this._runAsync((plan) => addon.extractWavAsync(plan, wavBytes, names, channel | 0));
   }
 
   static readWav(wavBytes) {
@@ -290,7 +305,8 @@ class Meyda {
   // addon keeps it alive until the job settles and the GC then frees it.
   dispose() {
     const all = Object.values(this._plans);
-    for (const pool of Object.values(this._asyncPlans)) all.push(...pool);
+    // (a pooled plan with jobs still queued on it is left to them, like a busy one)
+    for (const pool of Object.values(this._asyncPlans)) all.push(...pool.filter((sl) => sl.pending === 0).map((sl) => sl.plan));
     for (const p of all) if (!addon.planBusy(p)) addon.destroyPlan(p);
     this._plans = {};
     this._asyncPlans = {};

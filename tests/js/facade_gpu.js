@@ -196,6 +196,20 @@ check('async batch jobs run on their own plan: streaming continues meanwhile', (
   });
 });
 
+check('async jobs beyond the pool queue on its plans (at most options.asyncPlans per window)', () => {
+  const m = new Meyda(ctx, null, 512, null, { asyncPlans: 2 });
+  const F = 48;
+  const jobs = [];
+  for (let k = 0; k < 6; k++) jobs.push(m.getBatchAsync(['zcr', 'rms'], g.input.subarray(k * 512, (k + F) * 512)));
+  assert.ok(m._asyncPlans.hanning.length <= 2, 'pool grew to ' + m._asyncPlans.hanning.length);
+  return Promise.all(jobs).then((rs) => {
+    rs.forEach((r, k) => {
+      for (let i = 0; i < F; i++) assert.strictEqual(r.zcr[i], g.scalars[(k + i) * S + 2]);
+    });
+    m.dispose();
+  });
+});
+
 check('plan handle collected while an async job runs (no use-after-free)', () => {
   assert.ok(typeof global.gc === 'function', 'run node with --expose-gc');
   const x = g.input.subarray(0, 90 * 512);

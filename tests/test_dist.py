@@ -1,9 +1,13 @@
-"""Multi-process tests of the frame sharding and the feature gather (CPU, gloo, world 2).
+"""Multi-process tests of the multi-GPU run's host side (CPU, gloo, world 2).
 
-The GPU extraction itself cannot run here; each rank computes its shard's features
-with the CPU oracle as the stand-in producer, and rank 0 checks that the gathered
-SoA record equals one single-process extraction of the whole batch. This is the
-same code path bench.py / the GPU job use (meyda_amd.dist), minus the device.
+The GPU extraction and RCCL cannot run here. The world-2 test replays group.cpp's gather
+protocol between two real processes: each rank extracts its shard of one global stream
+(the CPU oracle stands in for the kernel), cuts it into the same chunks (mgx_shard_range),
+packs each chunk into one transfer buffer (mgx_packed_layout) and sends it to rank 0 with
+point-to-point messages (gloo send/recv in place of ncclSend/ncclRecv); rank 0 unpacks
+every chunk into its record and checks it against one extraction of the whole batch. The
+topology checks are bench.py's own (resolve_topology), which fail a run instead of
+measuring fewer GPUs than asked.
 """
 import os
 import socket
@@ -37,46 +41,101 @@ def test_shard_range_covers_exactly():
         shard_range(10, 2, 2)
 
 
-def _worker(rank, world, port, total, n, q):
+def test_bench_topology_fails_loudly():
+    sys.path.insert(0, ROOT)
+    import bench
+    rt = bench.resolve_topology
+    assert rt(None, {}, 8) == ("one", 1)
+    assert rt(4, {}, 8) == ("single", 4)
+    assert rt(None, {"WORLD_SIZE": "8"}, 8) == ("torchrun", 8)
+    assert rt(8, {"WORLD_SIZE": "8", "LOCAL_WORLD_SIZE": "8"}, 8) == ("torchrun", 8)
+    assert rt(1, {"WORLD_SIZE": "1"}, 1) == ("one", 1)
+    with pytest.raises(SystemExit, match="GPU"):
+        rt(2, {}, 1)  # a 1-GPU box asked for 2: no silent n_gpus 1
+    with pytest.raises(SystemExit, match="WORLD_SIZE"):
+        rt(8, {"WORLD_SIZE": "4"}, 8)
+    with pytest.raises(SystemExit, match="one GPU per rank"):
+        rt(2, {"WORLD_SIZE": "2", "LOCAL_WORLD_SIZE": "2"}, 1)
+    assert rt(2, {"WORLD_SIZE": "2", "LOCAL_WORLD_SIZE": "2"}, 1, allow_shared=True) == ("torchrun", 2)
+
+
+def _pack(capi, d, mask, ref, sl, cn):
+    """One chunk's transfer buffer, laid out by mgx_packed_layout (what the kernel writes)."""
+    nbytes, off = capi.packed_layout(d, mask, cn)
+    buf = np.zeros(nbytes, np.uint8)
+    for j, k in enumerate(capi.SCALAR_NAMES):
+        buf[off[k]:off[k] + 4 * cn] = ref["scalars"][sl, j].astype(np.float32).view(np.uint8)
+    for k, src in (("loudness.specific", ref["loudness_specific"]), ("mfcc", ref["mfcc"])):
+        b = np.ascontiguousarray(src[sl]).view(np.uint8).ravel()
+        buf[off[k]:off[k] + b.size] = b
+    return buf
+
+
+def _worker(rank, world, port, total, n, nch, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     sys.path.insert(0, ROOT)
     try:
-        from meyda_amd import SEED
-        from meyda_amd.dist import gather_features, init, shard_range
+        import torch.distributed as dist
+        from meyda_amd import SEED, capi
+        from meyda_amd.dist import init_control_plane
         from oracle import oracle
-        r, _, w = init(backend="gloo")
+        r, _, w = init_control_plane()
         assert (r, w) == (rank, world)
-        start, count = shard_range(total, world, rank)
-        x = oracle.synth_frames(SEED, start, count, n)  # this rank's shard of the global stream
+        d = capi.make_desc(buffer_size=n)
+        mask = (1 << 13) - 1 | capi.OUT_LOUDNESS_SPECIFIC | capi.OUT_MFCC
+        counts = [capi.shard_range(total, world, i)[1] for i in range(world)]
+        starts = [capi.shard_range(total, world, i)[0] for i in range(world)]
+        x = oracle.synth_frames(SEED, starts[rank], counts[rank], n)  # this rank's shard of the global stream
         ref = oracle.extract(x)
-        outs = {"scalars": torch.from_numpy(np.ascontiguousarray(ref["scalars"])),
-                "mfcc": torch.from_numpy(np.ascontiguousarray(ref["mfcc"])),
-                "loudness.specific": torch.from_numpy(np.ascontiguousarray(ref["loudness_specific"]))}
-        counts = [shard_range(total, world, i)[1] for i in range(world)]
-        got = gather_features(outs, counts, dst=0)
         if rank == 0:
+            rec = {"scalars": np.full((total, 13), np.nan, np.float32),
+                   "loudness.specific": np.full((total, 24), np.nan, np.float32),
+                   "mfcc": np.full((total, 13), np.nan, np.float32)}
+            c0s = [capi.shard_range(counts[0], nch, c) for c in range(nch)]
+            for c0, cn in c0s:  # the root's own shard in place
+                rec["scalars"][c0:c0 + cn] = ref["scalars"][c0:c0 + cn]
+                rec["loudness.specific"][c0:c0 + cn] = ref["loudness_specific"][c0:c0 + cn]
+                rec["mfcc"][c0:c0 + cn] = ref["mfcc"][c0:c0 + cn]
+            for c in range(nch):
+                for p in range(1, world):
+                    c0, cn = capi.shard_range(counts[p], nch, c)
+                    if not cn:
+                        continue
+                    nbytes, off = capi.packed_layout(d, mask, cn)
+                    t = torch.empty(nbytes, dtype=torch.uint8)
+                    dist.recv(t, src=p)  # ncclRecv into the staging slot
+                    buf = t.numpy()
+                    dst = slice(starts[p] + c0, starts[p] + c0 + cn)
+                    for j, k in enumerate(capi.SCALAR_NAMES):  # unpack_kernel's segments
+                        rec["scalars"][dst, j] = buf[off[k]:off[k] + 4 * cn].view(np.float32)
+                    for k in ("loudness.specific", "mfcc"):
+                        wdt = rec[k].shape[1]
+                        rec[k][dst] = buf[off[k]:off[k] + 4 * wdt * cn].view(np.float32).reshape(cn, wdt)
             whole = oracle.extract(oracle.synth_frames(SEED, 0, total, n))
-            ok = (np.array_equal(got["scalars"].numpy(), whole["scalars"], equal_nan=True)
-                  and np.array_equal(got["mfcc"].numpy(), whole["mfcc"], equal_nan=True)
-                  and np.array_equal(got["loudness.specific"].numpy(), whole["loudness_specific"], equal_nan=True)
-                  and got["scalars"].shape[0] == total)
+            ok = (np.array_equal(rec["scalars"], whole["scalars"].astype(np.float32), equal_nan=True)
+                  and np.array_equal(rec["mfcc"], whole["mfcc"], equal_nan=True)
+                  and np.array_equal(rec["loudness.specific"], whole["loudness_specific"], equal_nan=True))
             q.put(("ok" if ok else "mismatch", rank))
         else:
-            q.put(("ok" if got is None else "unexpected result", rank))
-        torch.distributed.barrier()
-        torch.distributed.destroy_process_group()
+            for c in range(nch):
+                c0, cn = capi.shard_range(counts[rank], nch, c)
+                if cn:  # ncclSend of the chunk's packed buffer
+                    dist.send(torch.from_numpy(_pack(capi, d, mask, ref, slice(c0, c0 + cn), cn)), dst=0)
+            q.put(("ok", rank))
+        dist.barrier()
+        dist.destroy_process_group()
     except Exception as e:  # report instead of hanging the parent
         q.put(("error: %r" % (e,), rank))
 
 
-@pytest.mark.parametrize("total", [64, 67])  # even and ragged shards
-def test_gather_world2_matches_single_process(total):
+@pytest.mark.parametrize("total,nch", [(64, 1), (67, 3), (40, 8)])  # even and ragged shards, chunk counts
+def test_gather_protocol_world2_matches_single_process(total, nch):
     world, n = 2, 512
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, total, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total, n, nch, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]

@@ -1,6 +1,6 @@
 """BASELINE config C5 on one GPU: the per-GPU shard of the 8-GPU job (262,144 frames of
-bufferSize = 2048, every feature including MFCC), synthesised in HBM, plus the RCCL
-gather of kernel-produced feature records.
+bufferSize = 2048, every feature including MFCC), synthesised in HBM. (The RCCL gather of
+the sharded records is tests/test_gpu_group.py::test_rccl_transport_group_gather.)
 
 Reference path: lib/jsfft/fft.js:123-171 at N = 2048 (widths up to 1024), the extractors
 src/extractors/*.js, and the per-buffer independence that makes frame sharding legal
@@ -8,9 +8,6 @@ src/extractors/*.js, and the per-buffer independence that makes frame sharding l
 bars); the whole shard through size-independent properties and launch-to-launch
 determinism.
 """
-import os
-import socket
-
 import numpy as np
 import pytest
 
@@ -73,37 +70,3 @@ def test_c5_shard_2048_all_features(capi, oracle_mod):
     torch.cuda.synchronize()
     for k in ("amplitudeSpectrum", "mfcc", "spectralRolloff", "loudness.specific"):
         assert torch.equal(out2[k], out[k]), k
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def test_rccl_gather_of_kernel_outputs(capi, oracle_mod):
-    """meyda_amd.dist.gather_features on the RCCL ("nccl") backend, world size 1, fed by the
-    HIP kernel's own outputs: the gathered record is byte-identical to the extraction."""
-    import torch
-    import torch.distributed as dist
-    from meyda_amd import dist as mdist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
-                      LOCAL_RANK="0")
-    n, F = 2048, 4096
-    frames = torch.empty(F, n, dtype=torch.float32, device="cuda")
-    capi.synth_frames_device(frames, SEED)
-    plan = capi.Plan(buffer_size=n)
-    out = plan.extract_torch(frames, ["rms", "spectralCentroid", "loudness", "mfcc"])
-    torch.cuda.synchronize()
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    try:
-        assert dist.get_backend() == "nccl"
-        got = mdist.gather_features(out, [F], dst=0)
-        torch.cuda.synchronize()
-    finally:
-        dist.destroy_process_group()
-    assert sorted(got) == sorted(out)
-    for k in out:
-        assert torch.equal(got[k], out[k]), k
-    ref = oracle_mod.extract(frames[:8].cpu().numpy())
-    assert np.allclose(got["rms"][:8].cpu().numpy(), ref["scalars"][:, 0], rtol=1e-5)

@@ -40,6 +40,7 @@ def test_one_rank_group_equals_plan(capi, mode, nch):
     want = plan.extract_torch(x, FEATS)
     if mode == "devices":
         g = capi.Group(buffer_size=n, devices=[0], scalar_f64=True)
+        assert g.comm_info() == (-1, -1, -1)  # one rank: no communicator
     else:
         g = capi.Group(buffer_size=n, rank=0, nranks=1, device=0, scalar_f64=True)
     assert (g.nranks, g.first_local, g.num_local) == (1, 0, 1)
@@ -133,6 +134,67 @@ def test_loopback_group_gather(capi, ranks, nch):
             a = got[k].view(torch.int32) if got[k].dtype == torch.float32 else got[k].view(torch.int64)
             b = want[k].view(torch.int32) if want[k].dtype == torch.float32 else want[k].view(torch.int64)
             assert torch.equal(a, b), (k, seed_shift)
+    g.close()
+
+
+@pytest.mark.parametrize("ranks,nch,n", [(2, 1, 1024), (3, 8, 1024), (4, 3, 2048)])
+def test_rccl_transport_group_gather(capi, ranks, nch, n):
+    """The RCCL transport on one GPU (mgx_group_create_loopback_rccl): every peer chunk crosses
+    as ncclSend / ncclRecv on a one-rank communicator (to and from itself) through group.cpp's
+    chunk loop, transfer slots and root unpack. The gathered record must be byte-identical to
+    one plan's extraction, for two calls on different frames, and the communicator must
+    report itself (one rank, rank 0, this device)."""
+    import torch
+    F = 40001 if n == 1024 else 20011
+    g = capi.Group(buffer_size=n, loopback=ranks, transport="rccl", scalar_f64=True)
+    assert (g.nranks, g.first_local, g.num_local) == (ranks, 0, ranks)
+    assert g.comm_info() == (1, 0, torch.cuda.current_device())
+    counts = [capi.shard_range(F, ranks, r)[1] for r in range(ranks)]
+    starts = [capi.shard_range(F, ranks, r)[0] for r in range(ranks)]
+    plan = capi.Plan(buffer_size=n, scalar_f64=True)
+    got, o = plan.alloc_outputs(F, FEATS)
+    stream = torch.cuda.current_stream().cuda_stream
+    for seed_shift in (0, 7919):
+        xs = [_frames(capi, c, n, first=s + seed_shift) for s, c in zip(starts, counts)]
+        for v in got.values():
+            v.fill_(float("nan"))
+        g.extract_device([t.data_ptr() for t in xs], counts, o, capi.output_mask(o), num_chunks=nch,
+                         streams=[stream] * ranks)
+        torch.cuda.synchronize()
+        want = plan.extract_torch(_frames(capi, F, n, first=seed_shift), FEATS)
+        torch.cuda.synchronize()
+        for k in want:
+            a = got[k].view(torch.int32) if got[k].dtype == torch.float32 else got[k].view(torch.int64)
+            b = want[k].view(torch.int32) if want[k].dtype == torch.float32 else want[k].view(torch.int64)
+            assert torch.equal(a, b), (k, seed_shift)
+    g.close()
+
+
+def test_rccl_transport_pipelined_steps(capi):
+    """bench.py's multi-rank step shape on the RCCL transport: consecutive group calls
+    alternating between two streams and two output sets, no host wait between them."""
+    import torch
+    n, F, ranks = 1024, 65536 + 7, 3
+    g = capi.Group(buffer_size=n, loopback=ranks, transport="rccl")
+    counts = [capi.shard_range(F, ranks, r)[1] for r in range(ranks)]
+    starts = [capi.shard_range(F, ranks, r)[0] for r in range(ranks)]
+    plan = capi.Plan(buffer_size=n)
+    feats = capi.ALL_FEATURES
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    calls = []
+    for shift in (0, 104729, 7919, 31):
+        got, o = plan.alloc_outputs(F, feats)
+        calls.append((shift, got, o, [_frames(capi, c, n, first=s + shift) for s, c in zip(starts, counts)]))
+    torch.cuda.synchronize()
+    for i, (_, _, o, xs) in enumerate(calls):
+        st = streams[i & 1].cuda_stream
+        g.extract_device([t.data_ptr() for t in xs], counts, o, capi.output_mask(o), num_chunks=8, streams=[st] * ranks)
+    torch.cuda.synchronize()
+    for shift, got, _, _ in calls:
+        want = plan.extract_torch(_frames(capi, F, n, first=shift), feats)
+        torch.cuda.synchronize()
+        for k in want:
+            assert torch.equal(got[k].view(torch.int32), want[k].view(torch.int32)), (k, shift)
     g.close()
 
 

@@ -59,12 +59,13 @@ def build(name, flags=()):
             raise SystemExit("%s: anchor found %d times: %r" % (name, src.count(old), old[:60]))
         src = src.replace(old, new)
     os.makedirs(os.path.join(ROOT, "abl"), exist_ok=True)
-    tmp = tempfile.NamedTemporaryFile("w", suffix=".hip", dir=SRC, prefix=".abl_", delete=False)
+    # the patched copy lives beside its library, outside the product source directory
+    tmp = tempfile.NamedTemporaryFile("w", suffix=".hip", dir=os.path.join(ROOT, "abl"), prefix=".abl_", delete=False)
     tmp.write(src)
     tmp.close()
     out = os.path.join(ROOT, "abl", "libabl_%s.so" % name)
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
-           "-mllvm", "-disable-machine-licm", *flags, "-shared", "-o", out, "-x", "hip", tmp.name,
+           "-mllvm", "-disable-machine-licm", "-I", SRC, *flags, "-shared", "-o", out, "-x", "hip", tmp.name,
            os.path.join(SRC, "plan.cpp"), os.path.join(SRC, "group.cpp"), "-ldl"]
     return subprocess.Popen(cmd), tmp.name, out
 
@@ -75,10 +76,17 @@ def main():
         names = list(PATCHES)
     jobs = [build(n) for n in names]
     rc = 0
-    for p, tmp, out in jobs:
-        rc |= p.wait()
-        os.unlink(tmp)
-        print(("built " if p.returncode == 0 else "FAILED ") + out)
+    try:
+        for p, tmp, out in jobs:
+            rc |= p.wait()
+            print(("built " if p.returncode == 0 else "FAILED ") + out)
+    finally:
+        for p, tmp, _ in jobs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+            if os.path.exists(tmp):
+                os.unlink(tmp)
     sys.exit(rc)
 
 
