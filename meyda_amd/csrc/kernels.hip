@@ -794,6 +794,18 @@ __device__ __forceinline__ __attribute__((address_space(1))) T* gbl(T* p) {
   return (__attribute__((address_space(1))) T*)p;
 }
 
+// A wave-uniform pointer passed through readfirstlane: loop strength reduction cannot then fold
+// a lane offset added later into a per-lane 64-bit induction variable. Such a variable (the
+// frame address, the complex output's) was carried across the batch loop in a VGPR pair and
+// spilled once per batch, and those scratch stores reached HBM: 128 B per frame, WRITE_SIZE
+// 1.8x the outputs. The loads and stores then take an SGPR base and a 32-bit lane offset.
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return (T*)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ int opaque(int v) {
   asm volatile("" : "+v"(v));
   return v;
@@ -1039,7 +1051,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   auto prefetch_next = [&]() {
     if constexpr (G::PF == 2) {
 #pragma unroll
-      for (int c = 0; c < CH; ++c) xn[c] = ld_frame(next + c * 64);
+      for (int c = 0; c < CH; ++c) xn[c] = ld_frame(next + (c * 64 + (unsigned)lane));
     }
   };
   if (!ap->need_spectrum) prefetch_next();  // time-only features: no table loads follow
@@ -1247,9 +1259,9 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       wave_sync();
       if (valid) {
         // complexSpectrum.js: the full N-point spectrum, X[N-k] = conj(X[k])
-        auto cr = gbl(ap->out.complex_real) + f * (uint64_t)N;
-        auto ci = gbl(ap->out.complex_imag) + f * (uint64_t)N;
-        for (int i = lane; i < N; i += 64) {
+        auto cr = uniform_ptr(gbl(ap->out.complex_real) + f * (uint64_t)N);
+        auto ci = uniform_ptr(gbl(ap->out.complex_imag) + f * (uint64_t)N);
+        for (unsigned i = lane; i < (unsigned)N; i += 64) {
           const float2 zz = i <= L ? buf[i] : buf[N - i];
           cr[i] = zz.x;
           ci[i] = i <= L ? zz.y : -zz.y;
@@ -1264,16 +1276,16 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   wave_sync();
 
   if (valid && ap->out.amplitude_spectrum) {
-    auto o = gbl(ap->out.amplitude_spectrum) + f * (uint64_t)L;
+    auto o = uniform_ptr(gbl(ap->out.amplitude_spectrum) + f * (uint64_t)L);
 #pragma unroll
-    for (int c = 0; c < R; ++c) o[c * 64 + lane] = amp[pa(c * 64 + lane)];
+    for (int c = 0; c < R; ++c) o[c * 64 + (unsigned)lane] = amp[pa(c * 64 + lane)];
   }
   if (valid && ap->out.power_spectrum) {
-    auto o = gbl(ap->out.power_spectrum) + f * (uint64_t)L;
+    auto o = uniform_ptr(gbl(ap->out.power_spectrum) + f * (uint64_t)L);
 #pragma unroll
     for (int c = 0; c < R; ++c) {
       const float av = amp[pa(c * 64 + lane)];
-      o[c * 64 + lane] = av * av;  // powerSpectrum.js
+      o[c * 64 + (unsigned)lane] = av * av;  // powerSpectrum.js
     }
   }
 
@@ -1742,12 +1754,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   auto frame_ptr = [&](uint64_t b, int j) {
     uint64_t f = b * FPW + j;
     f = f < nf ? f : nf - 1;
-    return (GF)(gbl(args_ptr()->frames) + f * (uint64_t)N + lane);
+    // (wave-uniform, uniform_ptr: the lane's offset is added at each load)
+    return (GF)uniform_ptr(gbl(args_ptr()->frames) + f * (uint64_t)N);
   };
   auto load = [&](float (&xv)[CH], uint64_t b, int j) {
     const GF xin = frame_ptr(b, j);
 #pragma unroll
-    for (int c = 0; c < CH; ++c) xv[c] = ld_frame(xin + c * 64);
+    for (int c = 0; c < CH; ++c) xv[c] = ld_frame(xin + (c * 64 + (unsigned)lane));
   };
 
   // the band lane's prefix-row offsets pd(lim[b]) | pd(lim[b + 1]) << 16 (G::BLIM_REG)
