@@ -75,11 +75,7 @@ struct Geo {
   static constexpr int RB = ilog2c(R);      // register bits
   static constexpr int NPASS = (SB + RB - 1) / RB;
   static constexpr int CH = N / 64;         // 64-sample input chunks per frame
-#ifndef MGX_FPW
   static constexpr int FPW = 4;             // frames per wave batch (phase 2 works on a wave batch)
-#else
-  static constexpr int FPW = MGX_FPW;
-#endif
   static constexpr int FB = 4 * FPW;        // frames per workgroup iteration
   // Register budget (VGPRs + AGPRs): 4 waves/SIMD (<= 128) up to N = 1024, where LDS
   // allows 4 workgroups per CU; 3 waves (<= 168) at N = 2048 (without the frame prefetch:
@@ -88,58 +84,30 @@ struct Geo {
   // N = 256 fits 6 waves (<= 80 VGPRs; measured 2.5 % faster than 5); at N = 512 a bound of
   // 5 waves measured slower than 4 until the LDS twiddles took the passes' global loads out
   // (81 VGPRs then, 3.9 % faster than 4 waves at 98).
-#ifndef MGX_WPE1024
-#define MGX_WPE1024 4
-#endif
-#ifndef MGX_WPE512
-#define MGX_WPE512 5
-#endif
-#ifdef MGX_WPE2048
-  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? MGX_WPE512 : N <= 1024 ? MGX_WPE1024 : MGX_WPE2048;
-#else
-  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? MGX_WPE512 : N <= 1024 ? MGX_WPE1024 : 3;
-#endif
+  static constexpr int WPE = N <= 256 ? 6 : N <= 512 ? 5 : N <= 1024 ? 4 : 3;
   // Slot buffer entries (8 bytes): the padded exchange image, the natural-order half
   // spectrum X[0..L] (complex output), the padded prefix row (pd) and the mel scratch.
   static constexpr int cmax(int a, int b) { return a > b ? a : b; }
   // (at N = 512 also room for the moment transpose, MOM_SLOT: 41 entries more than the FFT
   // needs, against the 11.5 KB table it replaces; the workgroup keeps 5 per CU with the
   // LDS twiddles)
-#ifndef MGX_SLOT_MOM512
-#define MGX_SLOT_MOM512 1
-#endif
   static constexpr int SLOT_PHYS =
       cmax(cmax(cmax(phys<N>(L - 1) + 1, L + 1), cmax(L + 2 * (L >> 5) + 1, 2 * (kMaxMel + 2 + 64) * 4 / 8)),
-           (N == 512 && MGX_SLOT_MOM512) ? 5 * 72 : 0);
+           N == 512 ? 5 * 72 : 0);
   // Moment sums through an LDS transpose (5 rows of 64 doubles per wave, row stride 72 so
   // the rows read together fall in different banks) rather than 5 DPP wave sums: measured
   // faster at every N (at 2048 once it ran in the slot buffer: a table of its own cost 3 waves
   // their LDS).
-#ifndef MGX_MOM_LDS_MAXN
-#define MGX_MOM_LDS_MAXN 2048  // (at 2048 through the slot buffer, MOM_SLOT: 1.5 % faster than DPP sums)
-#endif
-  static constexpr bool MOM_LDS = N <= MGX_MOM_LDS_MAXN;
+  // (at 2048 through the slot buffer, MOM_SLOT: 1.5 % faster than DPP sums)
+  static constexpr bool MOM_LDS = true;
   static constexpr int MOM_STRIDE = 72;
   // MOM_SLOT: the moment transpose runs in the wave's slot buffer right after the partials are
   // written (one more LDS round trip, no table of its own: 11.5 KB less LDS per workgroup)
-#ifndef MGX_MOM_SLOT
-#define MGX_MOM_SLOT 1
-#endif
-  static constexpr bool MOM_SLOT = MOM_LDS && MGX_MOM_SLOT && SLOT_PHYS >= 5 * MOM_STRIDE;
+  static constexpr bool MOM_SLOT = MOM_LDS && SLOT_PHYS >= 5 * MOM_STRIDE;
   // TW_LDS (N = 1024): the per-lane twiddles of passes >= 1 (the mixed-table entries and the
   // generic twiddles the tame passes read) are staged in LDS once per workgroup, in the space
   // the moment table left: LDS reads (lgkmcnt) instead of vector loads (vmcnt) in the passes
-#ifndef MGX_TW_LDS
-#define MGX_TW_LDS 1
-#endif
-#ifndef MGX_TW_LDS2048
-#define MGX_TW_LDS2048 1
-#endif
-#ifndef MGX_TW_LDS512
-#define MGX_TW_LDS512 1
-#endif
-  static constexpr bool TW_LDS = MGX_TW_LDS && ((N == 1024 && MOM_SLOT) || (N == 2048 && MGX_TW_LDS2048) ||
-                                                (N == 512 && MOM_SLOT && MGX_TW_LDS512));
+  static constexpr bool TW_LDS = (N == 1024 && MOM_SLOT) || N == 2048 || (N == 512 && MOM_SLOT);
   // Register prefetch of the next frame. A vector-memory wait is in issue order (vmcnt),
   // so a table load a frame waits on (window, twiddles) also waits for a prefetch issued
   // before it: prefetching at the start of the frame made every frame wait for the next
@@ -149,41 +117,20 @@ struct Geo {
   // this frame, after the last table loads this frame waits on (twiddles: the passes are
   // done; the mel records: issued just before), so no wait of this frame is held up by
   // it; PF = 0 loads each frame when its wave starts it.
-#ifdef MGX_PF_ALL
-  static constexpr int PF = MGX_PF_ALL;
-#else
-#ifndef MGX_PF1024
-#define MGX_PF1024 2
-#endif
-  static constexpr int PF = N <= 256 ? 1 : N < 1024 ? 2 : N == 1024 ? MGX_PF1024 : 0;  // measured best per N
-#endif
+  static constexpr int PF = N <= 256 ? 1 : N <= 1024 ? 2 : 0;  // measured best per N
   // WIN_REG: the window held in registers for the whole launch (CH VGPRs) instead of loaded
   // per frame (N = 1024, where the LDS twiddles freed the registers: 1.1-1.5 % faster, 119
-  // VGPRs; the frame prefetch at the frame's start instead, MGX_PF1024=1, 0.9-1.1 %, and both
+  // VGPRs; the frame prefetch at the frame's start instead, PF = 1, 0.9-1.1 %, and both
   // together 1.1 %)
-#ifndef MGX_WIN_REG
-#define MGX_WIN_REG 1
-#endif
-  static constexpr bool WIN_REG = MGX_WIN_REG && N == 1024;
+  static constexpr bool WIN_REG = N == 1024;
   // BLIM_REG: each band lane's two prefix-row offsets (bark limits, loudness.js:25-45) held in
   // one packed register for the launch instead of read from LDS per frame (N <= 512: -0.5 %;
   // at 1024 the register spills two others, +1.3 %; at 2048 a value kept live across the
   // frame loop spills)
-#ifndef MGX_BLIM_REG
-#define MGX_BLIM_REG 1
-#endif
-  static constexpr bool BLIM_REG = MGX_BLIM_REG && N <= 512;
+  static constexpr bool BLIM_REG = N <= 512;
   static constexpr bool PREFETCH = PF != 0;
-#ifdef MGX_LPREMAT
-  static constexpr bool LPREMAT = MGX_LPREMAT;
-#else
   static constexpr bool LPREMAT = N == 2048;  // measured: N = 2048 1 % faster, N = 256 7 % slower
-#endif
-#ifdef MGX_MIXFORM
-  static constexpr int MIX = MGX_MIXFORM;
-#else
   static constexpr int MIX = 1;  // bfly_mixed_tame (form 0 was faster at N = 1024 at 128 live VGPRs)
-#endif
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
 
@@ -278,7 +225,7 @@ __device__ __forceinline__ int pd(int d) { return d + (d >> 4); }
 // Wave priority (s_setprio) in the frame's low-ILP sections: a wave in an LDS round trip or a
 // serial chain (DPP reductions, the amplitude's conversions, phase 2's scalar steps) issues
 // ahead of the other waves, whose FFT passes have independent butterflies to fill the gaps,
-// so its latency overlaps their arithmetic instead of adding to it. MGX_PRIOSET selects the
+// so its latency overlaps their arithmetic instead of adding to it. kPrioSet selects the
 // regions: 1 the FFT exchanges, 2 the amplitude row's LDS round trip, 4 phase 2, 8 the
 // per-frame reductions (moment transpose, prefix and rolloff, band sums, mel scan), 16 the
 // frame start (energy/zcr, window, stage 0), 32 the amplitude, 64 the moment partials.
@@ -286,83 +233,38 @@ __device__ __forceinline__ int pd(int d) { return d + (d >> 4); }
 // 111 (all but the frame start, level 2) another 5.0 % at N = 1024, 4.3 % at 2048, 7.4 % at 512;
 // then levels: the exchanges and phase 2 at 3, the frame start at 1 (above the FFT's register
 // passes at 0), 127: another 1.4 % at 1024, 2.5 % at 2048, 2.1 % at 512.
-#ifndef MGX_PRIOSET
-#define MGX_PRIOSET 127
-#endif
-#ifndef MGX_PRIO_P2
-#define MGX_PRIO_P2 3
-#endif
-#ifndef MGX_PRIO_XCHG
-#define MGX_PRIO_XCHG 3
-#endif
-#ifndef MGX_PRIO_START
-#define MGX_PRIO_START 1
-#endif
-#ifndef MGX_PRIO_AMPROW
-#define MGX_PRIO_AMPROW 2
-#endif
-#ifndef MGX_PRIO_RED
-#define MGX_PRIO_RED 2
-#endif
-#ifndef MGX_PRIO_AMP
-#define MGX_PRIO_AMP 2
-#endif
-#ifndef MGX_PRIO_MOM
-#define MGX_PRIO_MOM 2
-#endif
+constexpr int kPrioSet = 127;  // every region: 1 | 2 | 4 | 8 | 16 | 32 | 64
+constexpr int prio_level(int region) {
+  return region == 4 ? 3 : region == 1 ? 3 : region == 16 ? 1 : 2;  // phase 2 and exchanges 3, frame start 1
+}
 template <int REGION>
 __device__ __forceinline__ void prio_hi() {
-  if constexpr ((MGX_PRIOSET & REGION) != 0)
-    __builtin_amdgcn_s_setprio(REGION == 4    ? MGX_PRIO_P2
-                               : REGION == 1  ? MGX_PRIO_XCHG
-                               : REGION == 16 ? MGX_PRIO_START
-                               : REGION == 2  ? MGX_PRIO_AMPROW
-                               : REGION == 8  ? MGX_PRIO_RED
-                               : REGION == 32 ? MGX_PRIO_AMP
-                                              : MGX_PRIO_MOM);
+  if constexpr ((kPrioSet & REGION) != 0) __builtin_amdgcn_s_setprio(prio_level(REGION));
 }
 template <int REGION>
 __device__ __forceinline__ void prio_lo() {
-  if constexpr ((MGX_PRIOSET & REGION) != 0) __builtin_amdgcn_s_setprio(0);
+  if constexpr ((kPrioSet & REGION) != 0) __builtin_amdgcn_s_setprio(0);
 }
 
 // pa(spectrum bin) of each register after the last pass, live across the whole frame loop:
-// two 16-bit entries per VGPR (MGX_KLPACK=0: one int per register; packed measured 1 %
-// faster at N = 512, 0.2 % at 1024).
-#ifndef MGX_KLPACK
-#define MGX_KLPACK 1
-#endif
+// two 16-bit entries per VGPR (packed measured 1 % faster than one int per register at
+// N = 512, 0.2 % at 1024).
 template <int N>
 struct KlTab {
   static constexpr int R = N / 128;
-#if MGX_KLPACK
   uint32_t w[R / 2];
   __device__ __forceinline__ void set(int r, int v) {
     if (r & 1) w[r >> 1] |= (uint32_t)v << 16;
     else w[r >> 1] = (uint32_t)v;
   }
   __device__ __forceinline__ int operator()(int r) const { return (int)((w[r >> 1] >> (16 * (r & 1))) & 0xFFFFu); }
-#else
-  int w[R];
-  __device__ __forceinline__ void set(int r, int v) { w[r] = v; }
-  __device__ __forceinline__ int operator()(int r) const { return w[r]; }
-#endif
 };
 
-// A frame sample: read once and never again. MGX_NT_FRAMES=1: non-temporal loads (`nt`).
-// Measured: the HBM-bound time-only features 12 % faster on a 1 GiB batch (5.9 TB/s), but
-// C2's 128 MiB batch 12 % slower (with plain loads it stays resident in the 256 MiB MALL
-// across launches); no change where the kernel is VALU-bound. Plain loads by default.
-#ifndef MGX_NT_FRAMES
-#define MGX_NT_FRAMES 0
-#endif
-__device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))) float* p) {
-#if MGX_NT_FRAMES
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
+// A frame sample: read once and never again. Plain loads: non-temporal ones (`nt`) took the
+// HBM-bound time-only features 12 % faster on a 1 GiB batch (5.9 TB/s), but C2's 128 MiB batch
+// 12 % slower (with plain loads it stays resident in the 256 MiB MALL across launches), and
+// made no change where the kernel is VALU-bound.
+__device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))) float* p) { return *p; }
 
 // Static instruction accounting (tools/isa_phases.py): -DMGX_MARKS puts an assembly comment
 // at each phase boundary; the default build has none.
@@ -679,10 +581,6 @@ __device__ __forceinline__ double wave_inclusive_scan(double v) {
   return v;
 }
 
-// MGX_AMP_MINMAX: the amplitude's per-slot range tests as one unsigned min/max per lane.
-#ifndef MGX_AMP_MINMAX
-#define MGX_AMP_MINMAX 1
-#endif
 
 // Amplitude of one slot: src/meyda.js:104-114, sqrt(re^2 + im^2) in double, stored to float32.
 template <bool FAITH>
@@ -1118,9 +1016,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     for (int c = 0; c < CH; ++c) e64 = __builtin_fma((double)x[c], (double)x[c], e64);
     e = wave_sum(e64);
   } else {
-#ifdef MGX_ENERGY_F64SUM
-    e = wave_sum((double)e32);
-#else
     // the 64 lane partials summed in float32 too (6 DPP-fused adds instead of 6 f64 DPP
     // steps): ~4e-7 relative at most on top of the partials' own ~1e-6, against the 1e-5 bar
     float t = e32;
@@ -1131,7 +1026,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     t += dpp_f<0x142, 0xA>(t);
     t += dpp_f<0x143, 0xC>(t);
     e = (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
-#endif
   }
   if (lane == 0) {
     recs[fb].energy = e;
@@ -1202,7 +1096,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
     float ar[R];
     if constexpr (FAITH) {
-#if MGX_AMP_MINMAX
       // The range test of every slot as one unsigned min and max of the float bits: each a is
       // >= +0 or NaN, so unsigned order is float order with NaN above +inf (caught by the max).
       uint32_t amin = 0xFFFFFFFFu, amax = 0u;
@@ -1217,17 +1110,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
         amax = max(amax, b);
       }
       const bool ok = amin >= __builtin_bit_cast(uint32_t, 0x1p-40f) && amax <= __builtin_bit_cast(uint32_t, 0x1p60f);
-#else
-      bool ok = true;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        bool okr;
-        ar[r] = slot_amp_rsq(v[r].x, v[r].y, okr);
-        // (the packed DC/Nyquist slot is replaced below: its range does not matter)
-        if (PG::rpart(G::NPASS - 1, r) == 0) okr = okr || dc_lane;
-        ok = ok && okr;
-      }
-#endif
       if (__ballot(!ok)) {  // a zero, tiny, huge or non-finite |X|^2 somewhere in the frame
 #pragma unroll
         for (int r = 0; r < R; ++r) ar[r] = slot_amp<FAITH>(v[r].x, v[r].y);

@@ -16,22 +16,16 @@ SRC = os.path.join(ROOT, "meyda_amd", "csrc")
 PATCHES = {
     "no_phase2": [("    MGX_MARK(phase2_start);\n    prio_hi<4>();\n    {", "    MGX_MARK(phase2_start);\n    prio_hi<4>();\n    if (opaque(0)) {\n    {"),
                   ("    prio_lo<4>();\n    MGX_MARK(phase2_end);", "    }\n    prio_lo<4>();\n    MGX_MARK(phase2_end);")],
-    "no_loud2": [("if (q->need_spectrum && q->need_loudness) {", "if (opaque(0) && q->need_spectrum && q->need_loudness) {")],
+    "no_loud2": [("if (!LIGHT && q->need_spectrum && q->need_loudness) {", "if (opaque(0) && !LIGHT && q->need_spectrum && q->need_loudness) {")],
     "no_ln": [("if (q->need_spectrum && q->need_mfcc) {\n        // mfcc.js:64",
                "if (opaque(0) && q->need_spectrum && q->need_mfcc) {\n        // mfcc.js:64")],
     "no_dct": [("if (q->need_spectrum && q->need_mfcc) {\n        const int nc",
                 "if (opaque(0) && q->need_spectrum && q->need_mfcc) {\n        const int nc")],
-    "no_scalars": [("for (int i = l2; i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {",
-                    "for (int i = l2; opaque(0) && i < MGX_LOUDNESS_TOTAL * FPW; i += 64) {")],
+    "no_scalars": [("for (int i = l2; i < (MGX_PERCEPTUAL_SHARPNESS + 1) * FPW; i += 64) {",
+                    "for (int i = l2; opaque(0) && i < (MGX_PERCEPTUAL_SHARPNESS + 1) * FPW; i += 64) {")],
     # the frame samples from the address instead of HBM (is the frame load's latency exposed?)
-    "no_frame_load": [("""#else
-  return *p;
-#endif
-}""", """#else
-  const uint32_t a = (uint32_t)(uintptr_t)p;
-  return (float)((a >> 2) & 1023) * 0x1p-10f - 0.5f;
-#endif
-}""")],
+    "no_frame_load": [("float* p) { return *p; }",
+                       "float* p) { const uint32_t a = (uint32_t)(uintptr_t)p; return (float)((a >> 2) & 1023) * 0x1p-10f - 0.5f; }")],
     # the per-lane twiddle loads of passes >= 1 made lane-uniform scalar loads
     "twuni": [("""__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
   const GD q = (GD)p;""", """__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
@@ -41,12 +35,12 @@ PATCHES = {
     "no_window_load": [("    for (int c = 0; c < CH; ++c) wv[c] = w[c * 64 + lane];",
                         "    for (int c = 0; c < CH; ++c) wv[c] = 0.5f + 0.25f * (c & 1);")],
     # (not an ablation: the DPP wave sums instead of the LDS transpose for the moments at N = 1024)
-    "mom_dpp": [("#define MGX_MOM_LDS_MAXN 2048", "#define MGX_MOM_LDS_MAXN 512")],
+    "mom_dpp": [("  static constexpr bool MOM_LDS = true;", "  static constexpr bool MOM_LDS = N <= 512;")],
     # the amplitude as |re| + |im| (no f64 squares, no rsq/Heron step)
     "no_amp": [("        ar[r] = slot_amp_rsq(v[r].x, v[r].y, okr);\n        uint32_t b",
                 "        ar[r] = fabsf(v[r].x) + fabsf(v[r].y); okr = true;\n        uint32_t b")],
     # the prefix row (stores, rolloff ballots) skipped: band sums read stale LDS
-    "no_prefix": [("  const bool need_prefix = SUB ? (bool)ap->need_prefix : true;",
+    "no_prefix": [("  const bool need_prefix = LIGHT ? false : SUB ? (bool)ap->need_prefix : true;",
                    "  const bool need_prefix = opaque(0);")],
     "no_mel": [("  } else if (ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && ap->need_mfcc) {\n    mel_energies")],
 }
