@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--frames", type=int, default=262144, help="frames per GPU per step")
     ap.add_argument("--precision", default="faithful", choices=["faithful", "fast"])
+    ap.add_argument("--single-stream", action="store_true",
+                    help="every step on one stream (no pipelining): a rocprofv3 --stats run of this command then "
+                         "averages whole, non-overlapping launches (profiles/*_kernel_stats.csv)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     ap.add_argument("--cpu-seconds", type=float, default=6.0,
@@ -147,15 +150,16 @@ class Devices:
     stream's first launches carry a one-time cost of milliseconds (its hardware queue), which
     settle() absorbs."""
 
-    def __init__(self, devs):
+    def __init__(self, devs, single=False):
         self.devs = list(devs)
+        self.single = single  # --single-stream: every step on stream 0 (launches never overlap)
         self.streams = {}
         for d in self.devs:
             with torch.cuda.device(d):
                 self.streams[d] = [torch.cuda.current_stream(d), torch.cuda.Stream(device=d)]
 
     def stream(self, d, k):
-        return self.streams[d][k & 1]
+        return self.streams[d][0 if self.single else k & 1]
 
     def sync(self):
         for d in self.devs:
@@ -376,9 +380,9 @@ def main():
         import torch.distributed as tdist
         mdist.init_control_plane()  # gloo: control plane only; the data path is the library's RCCL gather
         dist = tdist
-        devs = Devices([local % torch.cuda.device_count()])
+        devs = Devices([local % torch.cuda.device_count()], args.single_stream)
     else:
-        devs = Devices(range(gpus))
+        devs = Devices(range(gpus), args.single_stream)
     torch.cuda.set_device(devs.devs[0])
     # which GPU every rank / local device is (the driver's node: one each)
     me = [{"rank": rank + i, "device": d, "uuid": str(torch.cuda.get_device_properties(d).uuid),
@@ -490,9 +494,11 @@ def secondary(args, plan, frames, devs, n, F):
             p.extract_device(frames.data_ptr(), F, sets[k & 1][1], devs.stream(dev, k).cuda_stream)
         settle(st, devs, args.settle_ms)
         el, km, stats = run_mode(st, devs, args.steps, args.warmup, None)
-        return {"value": F * args.steps / el, "unit": "frames/s", "kernel_ms": km,
-                "kernel_ms_launch_alone": stats["launch_alone_median_ms"], "bytes_per_frame": bytes_per_frame,
-                "roofline_frac": F * bytes_per_frame / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        alone = stats["launch_alone_mean_ms"]
+        return {"value": F * args.steps / el, "unit": "frames/s", "kernel_ms": alone, "period_ms": km,
+                "bytes_per_frame": bytes_per_frame,
+                "roofline_frac": F * bytes_per_frame / (alone * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "frac_pipelined": F * bytes_per_frame / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
     if not args.no_fast and args.precision != "fast":
         # the fp32-butterfly mode beside the faithful one (same features and frames)
         out["fast_mode"] = dict(timed(capi.Plan(buffer_size=n, precision="fast", device=dev), FEATURES,
@@ -529,21 +535,24 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
     use_gather = gather is not None and gather.get("status") == "ok"
     value = gather["value"] if use_gather else value_s
     elapsed = args.steps * 1e3 / (value / (gpus * F))  # ms for the K steps
-    kernel_ms = km_s  # the shards' launch period: the roofline of the extraction kernel
-    alone_ms = (stats_s["rank0"] if "rank0" in stats_s else stats_s)["launch_alone_median_ms"]
+    # the roofline of the extraction kernel: its average launch duration, launches serialised on one
+    # stream with an event pair around each (what rocprofv3 --stats reports per dispatch); the
+    # launch period of the pipelined timed steps (value) is reported beside it
+    alone_ms = (stats_s["rank0"] if "rank0" in stats_s else stats_s)["launch_alone_mean_ms"]
+    kernel_ms = alone_ms
     achieved = F * bytes_per_frame / (kernel_ms * 1e-3) / 1e9
     traffic, valu, traffic_note = extras.get("pmc") or (None, None, "not measured (--no-pmc or N > 1)")
     if valu is not None:
         # the faithful path is FP64-VALU bound. Issue costs per wave64
         # instruction measured by tools/ubench/op_rates.hip (profiles/r01_op_rates.log):
         # f64 ~5.0, f32<->f64 conversion 4.2 cycles; at the clock this run's kernel time implies
-        cyc = kernel_ms * 1e-3 * 2.4e9 * 1024 / F  # SIMD cycles per frame (2.4 GHz held, 1,024 SIMDs)
+        cyc = km_s * 1e-3 * 2.4e9 * 1024 / F  # SIMD cycles per frame at the timed steps' rate (2.4 GHz, 1,024 SIMDs)
         valu["frame_simd_cycles"] = cyc
         valu["est_fp64_cvt_busy"] = (valu["f64_per_frame"] * 5.0 + valu["cvt_per_frame"] * 4.2) / cyc
         # FP64 pipe (vector and matrix share it): 78.6 TFLOP/s dense on MI355X (1,024 SIMDs x 32
         # FLOP/clk x 2.4 GHz; v_mfma_f64_4x4x4 issues every 16 cycles: tools/ubench/op_rates.hip)
         mf = valu["mfma_f64"]
-        mf["tflops"] = mf["flop_per_launch"] / (kernel_ms * 1e-3) / 1e12
+        mf["tflops"] = mf["flop_per_launch"] / (km_s * 1e-3) / 1e12
         mf["peak_tflops"] = 78.6
         mf["frac"] = mf["tflops"] / mf["peak_tflops"]
     line = {
@@ -574,9 +583,13 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                      "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
-                     "kernel_ms_source": "launch period: HIP events around the timed region / steps "
-                                         "(steps pipelined over two streams); a launch on its own: step_event_ms",
-                     "frac_launch_alone": F * bytes_per_frame / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "kernel_ms_source": "mean launch duration: 20 launches serialised on one stream after the "
+                                         "timed steps, an event pair around each (rocprofv3 --stats of "
+                                         "bench.py --single-stream: profiles/)",
+                     "period_ms": km_s,
+                     "period_source": ("launch period of the timed steps: HIP events around the timed region / steps"
+                                       + (" (one stream)" if args.single_stream else " (steps pipelined over two streams)")),
+                     "frac_pipelined": F * bytes_per_frame / (km_s * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "step_event_ms": stats_s,
                      "bytes_per_frame": bytes_per_frame},
     }
