@@ -134,6 +134,17 @@ struct Geo {
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
 
+// The kernel instances with the mel sums as chains in the reference's order (CHAIN:
+// MGX_FLAG_MFCC_REFERENCE at N <= 1024, mel_chains) hold the batch's power rows in LDS (3 rows
+// per wave; the 4th in the slot buffer): at N = 1024 the tame passes' twiddles leave the LDS
+// for them and the workgroups per CU go from 4 to 3 (so the register bound from 128 to 168).
+template <int N, bool CHAIN>
+struct KGeo {
+  static constexpr bool TW_LDS = Geo<N>::TW_LDS && !(CHAIN && N == 1024);
+  static constexpr int WPE = !CHAIN ? Geo<N>::WPE : N <= 256 ? 5 : N <= 512 ? 4 : 3;
+  static constexpr int ROWS = CHAIN ? 3 : 0;  // power rows per wave in LDS of their own
+};
+
 // Location bits of pass p: register bits [0, m) drive location bits [q0, q0+m); the
 // six lane bits take the lowest remaining location bits; leftover register bits
 // take the rest. Pass 0 is fixed by the load: location = rev6(lane)*R + r.
@@ -460,10 +471,10 @@ __device__ __forceinline__ void bfly_mixed_tame(float2& lo, float2& hi, double2 
 // amplitude changes had freed registers; before, 1.8 % slower).
 
 // One radix-2 stage on location bit q = q0(P) + I, entirely in registers.
-template <int N, int P, int I, bool FAITH, bool TAME>
+template <int N, int P, int I, bool FAITH, bool TAME, bool TWL>
 __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm,
                                           const double2* twl) {
-  constexpr bool LT = FAITH && TAME && Geo<N>::TW_LDS && P > 0 && TwLds<N>::pass_lds(P);  // twiddles from the LDS image
+  constexpr bool LT = FAITH && TAME && TWL && P > 0 && TwLds<N>::pass_lds(P);  // twiddles from the LDS image
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int q = PG::q0(P) + I;
@@ -504,12 +515,12 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
   }
 }
 
-template <int N, int P, int I, bool FAITH, bool TAME>
+template <int N, int P, int I, bool FAITH, bool TAME, bool TWL>
 __device__ __forceinline__ void run_stages(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm,
                                            const double2* twl) {
   if constexpr (I < PassGeo<N>::m(P)) {
-    run_stage<N, P, I, FAITH, TAME>(v, lp, tw, twf, twm, twl);
-    run_stages<N, P, I + 1, FAITH, TAME>(v, lp, tw, twf, twm, twl);
+    run_stage<N, P, I, FAITH, TAME, TWL>(v, lp, tw, twf, twm, twl);
+    run_stages<N, P, I + 1, FAITH, TAME, TWL>(v, lp, tw, twf, twm, twl);
   }
 }
 
@@ -531,13 +542,13 @@ __device__ __forceinline__ void exchange(float2 (&v)[Geo<N>::R], int lp_prev, in
   MGX_MARK(xchg_end);
 }
 
-template <int N, int P, bool FAITH, bool TAME>
+template <int N, int P, bool FAITH, bool TAME, bool TWL>
 __device__ __forceinline__ void run_passes(float2 (&v)[Geo<N>::R], const int (&lp)[Geo<N>::NPASS],
                                            float2* buf, GTw tw, GTwf twf, GTw twm, const double2* twl) {
   if constexpr (P < Geo<N>::NPASS) {
     if constexpr (P > 0) exchange<N, P>(v, lp[P - 1], lp[P], buf);
-    run_stages<N, P, 0, FAITH, TAME>(v, lp[P], tw, twf, twm, twl);
-    run_passes<N, P + 1, FAITH, TAME>(v, lp, buf, tw, twf, twm, twl);
+    run_stages<N, P, 0, FAITH, TAME, TWL>(v, lp[P], tw, twf, twm, twl);
+    run_passes<N, P + 1, FAITH, TAME, TWL>(v, lp, buf, tw, twf, twm, twl);
   }
 }
 
@@ -714,7 +725,7 @@ __device__ __forceinline__ void put_scalar(KArgs* a, int i, uint64_t f, double v
   if (a->out.scalars[i]) gbl(static_cast<T*>(a->out.scalars[i]))[f] = (T)v;
 }
 
-template <int N>
+template <int N, bool CHAIN = false>
 struct Lds {
   using G = Geo<N>;
   // One slot buffer per wave: FFT exchanges, then the frame's amplitude row, its prefix
@@ -737,10 +748,13 @@ struct Lds {
   static constexpr size_t kc_bytes = 16 * 8 + 32 * 4;
   // The tame passes' per-lane twiddles (Geo<N>::TW_LDS, TwLds), staged once per workgroup.
   static constexpr size_t twl_off = kc_off + kc_bytes;
-  static constexpr size_t twl_bytes = G::TW_LDS ? (size_t)TwLds<N>::total() * 16 : 0;
+  static constexpr size_t twl_bytes = KGeo<N, CHAIN>::TW_LDS ? (size_t)TwLds<N>::total() * 16 : 0;
   static_assert(twl_off % 16 == 0, "double2 alignment");
+  // CHAIN: the power rows of the first three frames of each wave's batch (mel_chains).
+  static constexpr size_t rows_off = twl_off + twl_bytes;
+  static constexpr size_t rows_bytes = (size_t)4 * KGeo<N, CHAIN>::ROWS * G::L * 4;
   // The DCT table (mfcc.js:67-83), staged once per workgroup, sized per plan.
-  static constexpr size_t dct_off = twl_off + twl_bytes;
+  static constexpr size_t dct_off = rows_off + rows_bytes;
   static size_t bytes(int ncoef, int nfilt) { return dct_off + (size_t)ncoef * ((nfilt + 7) & ~7) * 4; }
 };
 
@@ -930,17 +944,55 @@ __device__ __forceinline__ void mel_reference_order(KArgs* ap, const float (&av)
   }
 }
 
+// MGX_FLAG_MFCC_REFERENCE at N <= 1024 (the CHAIN kernels): the mel band energies of the wave's
+// batch in the reference's own order (mfcc.js:53-62), over the 4 power rows phase 1 left in LDS.
+// Each band of each frame is one serial chain: from its first bin in ascending order, the weight
+// (an IEEE double quotient, plan table) times the float32 power rounded to double, added to the
+// Float32Array element in double and stored back to float32 -- exactly the reference's
+// operations, so the sums are the reference's bits. The host schedule (plan.cpp chain_schedule)
+// puts 64 chains side by side per phase, a band's 4 frames in one phase, every lane of a phase
+// running its length; the critical path is the longest band (120 bins at N = 1024 with 26 bands),
+// shared by the batch's 4 frames. Per step: one LDS read, one (cached) weight load, and the
+// conversion, product, sum and the two roundings on the VALU.
+template <int N>
+__device__ __forceinline__ void mel_chains(KArgs* q, int lane, const float* rows, const float* last, FrameRec* recs) {
+  constexpr int L = N / 2;
+  const auto cl = gbl(reinterpret_cast<const uint32_t*>(q->t.chain_lane));
+  const auto cw = gbl(q->t.chain_w);
+  for (int ph = 0; ph < q->chain_nph; ++ph) {
+    const uint32_t rx = cl[2 * (ph * 64 + lane)], ry = cl[2 * (ph * 64 + lane) + 1];
+    const int s0 = (int)(rx & 0xFFFu), fr = (int)((rx >> 12) & 3u), band = (int)((rx >> 16) & 0x7Fu);
+    const float* pr = (fr < Geo<N>::FPW - 1 ? rows + fr * L : last) + s0;
+    const auto wp = cw + ry;
+    const int len = q->chain_len[ph];
+    double acc = 0.0;  // the Float32Array element, held exactly in double
+    for (int s = 0; s < len; s += 8) {
+      float p[8];
+      double w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        p[u] = pr[s + u];
+        w[u] = wp[s + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = (double)(float)(acc + w[u] * (double)p[u]);  // two roundings, the float32 store
+    }
+    if ((int)rx < 0 && !(recs[fr].zcr & kChainSkip)) recs[fr].lm[band] = (float)acc;
+  }
+}
+
 // One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
-template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME>
+template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
                                              int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
                                              const int* klim, float (&xn)[Geo<N>::PREFETCH ? Geo<N>::CH : 1],
                                              GF next, const double2* twl, const float (&wreg)[Geo<N>::CH],
-                                             uint32_t blim) {
+                                             uint32_t blim, float* rows) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
+  constexpr bool TWL = KGeo<N, CHAIN>::TW_LDS;
   float* amp = reinterpret_cast<float*>(buf);  // the frame's amplitude row, once the FFT is done
   double* pbuf = reinterpret_cast<double*>(buf);
 
@@ -1083,12 +1135,12 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     for (int p = 0; p < G::NPASS; ++p) lpf[p] = G::LPREMAT ? PG::lanepart(p, opaque(lane)) : lp[p];
     if constexpr (FAITH) {
       // pass 0 has no mixed pairs; the later passes take the tame form when they can
-      run_stages<N, 0, 0, FAITH, false>(v, lpf[0], tw, twf, twm, twl);
+      run_stages<N, 0, 0, FAITH, false, TWL>(v, lpf[0], tw, twf, twm, twl);
       MGX_MARK(pass0_done);
-      if (tame) run_passes<N, 1, FAITH, true>(v, lpf, buf, tw, twf, twm, twl);
-      else run_passes<N, 1, FAITH, false>(v, lpf, buf, tw, twf, twm, twl);
+      if (tame) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);
+      else run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);
     } else {
-      run_passes<N, 0, FAITH, false>(v, lpf, buf, tw, twf, twm, twl);
+      run_passes<N, 0, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);
     }
     MGX_MARK(fft_done);
     prio_hi<32>();
@@ -1321,7 +1373,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // flight. (Issued any earlier, the extra live registers spill around the moment sums,
   // and a spill reload is a vector-memory wait behind the prefetch.)
   MelTab<N> mt;
-  if (ap->need_mfcc) mt.load(ap, lane);
+  if (!CHAIN && ap->need_mfcc) mt.load(ap, lane);
   prefetch_next();
   if (!kMomLds && need_mom) {
     const double S1 = wave_sum(P1);
@@ -1356,12 +1408,25 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // mel bands over all bins in reference order (mfcc.js:53-62).
   // (total = sum of the amplitudes in double: non-finite iff some amplitude is.)
   MGX_MARK(bands_done);
-  if (light ? light_nonfinite : !(total < __builtin_huge_val())) {
+  const bool nonfinite = light ? light_nonfinite : !(total < __builtin_huge_val());
+  if (nonfinite) {
     nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
-  } else if (SUB && ap->need_mfcc && ap->mfcc_reference) {  // (the all-feature kernel never has the flag)
+  } else if (!CHAIN && SUB && ap->need_mfcc && ap->mfcc_reference) {  // (N = 2048 only; the all-feature kernel never has the flag)
     mel_reference_order<N>(ap, av, lane, buf, rec);
-  } else if (ap->need_mfcc) {
+  } else if (!CHAIN && ap->need_mfcc) {
     mel_energies<N>(ap, av, lane, buf, rec, mt);
+  }
+  if constexpr (CHAIN) {
+    // the frame's power row (powerSpectrum.js) for the batch's mel chains in phase 2: the first
+    // three frames of the batch in rows of their own, the last in the slot buffer; a non-finite
+    // frame keeps the mel sums nonfinite_frame_sums formed (kChainSkip, a bit of its zcr count)
+    if (ap->need_mfcc) {
+      float* row = fb < Geo<N>::FPW - 1 ? rows + fb * L : amp;
+      wave_sync();  // the slot buffer's band-sum (and non-finite) reads are done
+#pragma unroll
+      for (int jj = 0; jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];
+      if (nonfinite && lane == 0) rec.zcr = rec.zcr | kChainSkip;
+    }
   }
   MGX_MARK(mel_done);
   if (kMomLds && !G::MOM_SLOT && need_mom) {
@@ -1462,7 +1527,7 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   switch (sc) {
     case MGX_RMS: num = rc.energy * (1.0 / N); break;  // rms.js: sqrt(sum / N), N a power of 2
     case MGX_ENERGY: num = rc.energy; break;           // energy.js
-    case MGX_ZCR: num = (double)rc.zcr; break;         // zcr.js
+    case MGX_ZCR: num = (double)(rc.zcr & (kChainSkip - 1)); break;  // zcr.js (the CHAIN kernels' flag bit masked)
     case MGX_SPECTRAL_CENTROID: num = m1; break;       // spectralCentroid.js
     case MGX_SPECTRAL_FLATNESS:                        // spectralFlatness.js: geometric / arithmetic mean
       num = SUB ? geo : exp2_mean(rc.ln2sum * (1.0 / L)) * L;
@@ -1523,11 +1588,11 @@ __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
 __device__ unsigned long long g_wave_times[65536 * 4];
 #endif
 
-template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
+template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N, CHAIN>::WPE))) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
-  using LY = Lds<N>;
+  using LY = Lds<N, CHAIN>;
   constexpr int R = G::R, CH = G::CH, FPW = G::FPW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
@@ -1538,6 +1603,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float2* buf = slot_all + wave * G::SLOT_PHYS;
   FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off) + wave * FPW;  // this wave's records
+  float* rows = reinterpret_cast<float*>(smem + LY::rows_off) + wave * KGeo<N, CHAIN>::ROWS * G::L;  // CHAIN: power rows
   KArgs* ap = args_ptr();
 #if MGX_WAVE_TIMES
   const unsigned long long wt0 = wall_clock64();
@@ -1550,7 +1616,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     if (threadIdx.x < MGX_NUM_SCALARS) kptr[threadIdx.x] = ap->out.scalars[threadIdx.x];
     if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = gbl(ap->t.bblim)[threadIdx.x - 64];
   }
-  if constexpr (G::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
+  if constexpr (KGeo<N, CHAIN>::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
     stage_twiddles<N, 1, 0>(reinterpret_cast<double2*>(smem + LY::twl_off), gbl(ap->t.tw), gbl(ap->t.twm));
   }
   if (ap->need_spectrum && ap->need_mfcc) {
@@ -1680,9 +1746,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       } else {
         load(x, b, j);
       }
-      frame_phase1<N, FAITH, LITERAL, SUB, LIGHT, NOTIME>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
+      frame_phase1<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
                                       reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
-                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim);
+                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim, rows);
     }
     wave_sync();
 
@@ -1691,6 +1757,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     // hoisted out of the batch loop (it would stay live across the FFT).
     MGX_MARK(phase2_start);
     prio_hi<4>();
+    if constexpr (CHAIN) {
+      KArgs* q = args_ptr();
+      if (q->need_spectrum && q->need_mfcc) {
+        mel_chains<N>(q, opaque(lane), rows, reinterpret_cast<const float*>(buf), recs);
+        wave_sync();  // the band energies are in the records: the log step reads them
+      }
+    }
     {
       KArgs* q = args_ptr();
       const int l2 = opaque(lane);
@@ -1736,7 +1809,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       if (q->need_spectrum && q->need_mfcc) {
         // mfcc.js:64 Math.log of the band energies, stored to Float32Array
         const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
-        const bool ref_log = SUB && q->mfcc_reference;  // the double Math.log, then float32
+        const bool ref_log = CHAIN || (SUB && q->mfcc_reference);  // the double Math.log, then float32
         // two bands per lane (a pair of adjacent floats: one LDS read and write each): the
         // batch's 4 frames x 32 bands in one pass
         auto ln1 = [&](float v, int band) {
@@ -1757,7 +1830,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       MGX_MARK(ln_done);
       if (q->need_spectrum && q->need_mfcc) {
         const int nc = q->ncoef, nfilt = q->nfilt;
-        if (q->dct_sequential || (SUB && q->mfcc_reference)) {
+        if (q->dct_sequential || (SUB && !CHAIN && q->mfcc_reference)) {
         // MGX_FLAG_DCT_SEQUENTIAL: VALU FMAs in the reference's sequential order, one lane per
         // (coefficient, frame). (The matrix-core form below is the default: 0.5 % faster for the
         // whole kernel and equal on every golden coefficient)
@@ -1880,32 +1953,43 @@ __global__ void unpack_kernel(UnpackArgs a) {
     dst[i] = src[i];
 }
 
-template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false>
+template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false, bool CHAIN = false>
 hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
-  const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
-  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME>), dim3(grid), dim3(kThreads), lds, stream, a);
+  const size_t lds = Lds<N, CHAIN>::bytes(a.ncoef, a.nfilt);
+  hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN>), dim3(grid), dim3(kThreads), lds, stream, a);
   return hipGetLastError();
 }
 
-template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false>
-int occupancy_n(size_t lds) {
+template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false, bool CHAIN = false>
+int occupancy_n(int ncoef, int nfilt) {
   int blocks = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME>, kThreads, lds) !=
-      hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN>, kThreads,
+                                                   Lds<N, CHAIN>::bytes(ncoef, nfilt)) != hipSuccess)
     return 0;
   return blocks;
 }
 
+// the instances a plan's launches use: MGX_FLAG_MFCC_REFERENCE at N <= 1024 takes the CHAIN pair
+// (all features / any subset), every other faithful plan the four below
 template <int N>
-int occupancy_prec(int precision, int mode, int ncoef, int nfilt) {
-  const size_t lds = Lds<N>::bytes(ncoef, nfilt);
-  if (mode == MGX_MODE_LITERAL) return occupancy_n<N, true, true>(lds);
-  if (precision == MGX_PRECISION_FAST) return occupancy_n<N, false, false>(lds);
+constexpr bool kChainN = N <= kChainMaxN;
+
+template <int N>
+int occupancy_prec(int precision, int mode, int ncoef, int nfilt, bool chain) {
+  if (mode == MGX_MODE_LITERAL) return occupancy_n<N, true, true>(ncoef, nfilt);
+  if (precision == MGX_PRECISION_FAST) return occupancy_n<N, false, false>(ncoef, nfilt);
+  if constexpr (kChainN<N>) {
+    if (chain) {
+      const int m = occupancy_n<N, true, false, false, false, false, true>(ncoef, nfilt),
+                o = occupancy_n<N, true, false, true, false, false, true>(ncoef, nfilt);
+      return o < m ? o : m;
+    }
+  }
   // the grid serves the four faithful kernels (all features / without the time-domain ones /
   // a subset / a light subset)
-  int m = occupancy_n<N, true, false>(lds);
-  for (int o : {occupancy_n<N, true, false, false, false, true>(lds), occupancy_n<N, true, false, true>(lds),
-                occupancy_n<N, true, false, true, true>(lds)})
+  int m = occupancy_n<N, true, false>(ncoef, nfilt);
+  for (int o : {occupancy_n<N, true, false, false, false, true>(ncoef, nfilt), occupancy_n<N, true, false, true>(ncoef, nfilt),
+                occupancy_n<N, true, false, true, true>(ncoef, nfilt)})
     m = o < m ? o : m;
   return m;
 }
@@ -1914,8 +1998,16 @@ template <int N>
 hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, hipStream_t stream) {
   if (mode == MGX_MODE_LITERAL) return launch_n<N, true, true>(a, grid, stream);
   if (precision == MGX_PRECISION_FAST) return launch_n<N, false, false>(a, grid, stream);
+  const bool every = a.need_mom == 2 && a.need_prefix && a.need_energy && a.need_zcr;
+  if constexpr (kChainN<N>) {
+    // MGX_FLAG_MFCC_REFERENCE: the mel sums as chains in the reference's order (mel_chains)
+    if (a.chain_nph > 0 && a.need_spectrum && a.need_mfcc) {
+      if (every) return launch_n<N, true, false, false, false, false, true>(a, grid, stream);
+      return launch_n<N, true, false, true, false, false, true>(a, grid, stream);
+    }
+  }
   // a spectral feature subset that skips the moment / prefix / time-domain work takes the SUB kernel
-  // (and so does MGX_FLAG_MFCC_REFERENCE: the all-feature kernel keeps its schedule)
+  // (and so does MGX_FLAG_MFCC_REFERENCE at N = 2048: mel_reference_order, one frame at a time)
   // (LIGHT: a subset reading neither the moments nor the prefix row, e.g. mfcc or the spectra
   // alone, compiled without that code: no runtime branches to keep its registers live)
   if (a.need_spectrum && a.need_mom == 0 && !a.need_prefix && !a.mfcc_reference)
@@ -1924,18 +2016,18 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
   // with the time-domain reductions compiled out)
   if (a.need_spectrum && a.need_mom == 2 && a.need_prefix && !a.need_energy && !a.need_zcr && !a.mfcc_reference)
     return launch_n<N, true, false, false, false, true>(a, grid, stream);
-  if (a.need_spectrum && (!(a.need_mom == 2 && a.need_prefix && a.need_energy && a.need_zcr) || a.mfcc_reference))
+  if (a.need_spectrum && (!every || a.mfcc_reference))
     return launch_n<N, true, false, true>(a, grid, stream);
   return launch_n<N, true, false>(a, grid, stream);
 }
 
 }  // namespace
 
-size_t extract_lds_bytes(int n, int ncoef, int nfilt) {
+size_t extract_lds_bytes(int n, int ncoef, int nfilt, bool chain) {
   switch (n) {
-    case 256: return Lds<256>::bytes(ncoef, nfilt);
-    case 512: return Lds<512>::bytes(ncoef, nfilt);
-    case 1024: return Lds<1024>::bytes(ncoef, nfilt);
+    case 256: return chain ? Lds<256, true>::bytes(ncoef, nfilt) : Lds<256>::bytes(ncoef, nfilt);
+    case 512: return chain ? Lds<512, true>::bytes(ncoef, nfilt) : Lds<512>::bytes(ncoef, nfilt);
+    case 1024: return chain ? Lds<1024, true>::bytes(ncoef, nfilt) : Lds<1024>::bytes(ncoef, nfilt);
     case 2048: return Lds<2048>::bytes(ncoef, nfilt);
     default: return 0;
   }
@@ -1951,12 +2043,12 @@ int frames_per_batch(int n) {
   }
 }
 
-int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt) {
+int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt, bool chain) {
   switch (n) {
-    case 256: return occupancy_prec<256>(precision, mode, ncoef, nfilt);
-    case 512: return occupancy_prec<512>(precision, mode, ncoef, nfilt);
-    case 1024: return occupancy_prec<1024>(precision, mode, ncoef, nfilt);
-    case 2048: return occupancy_prec<2048>(precision, mode, ncoef, nfilt);
+    case 256: return occupancy_prec<256>(precision, mode, ncoef, nfilt, chain);
+    case 512: return occupancy_prec<512>(precision, mode, ncoef, nfilt, chain);
+    case 1024: return occupancy_prec<1024>(precision, mode, ncoef, nfilt, chain);
+    case 2048: return occupancy_prec<2048>(precision, mode, ncoef, nfilt, false);
     default: return 0;
   }
 }

@@ -12,6 +12,11 @@ constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
 constexpr int kMelHead = kMaxMel + 2;  // mel scratch: segment sums [0, nfilt + 2), head partials from here
+// Mel band chains in the reference's own order (MGX_FLAG_MFCC_REFERENCE, N <= 1024): a wave
+// batch's 4 frames x nfilt chains, 64 per phase, so at most 4 phases.
+constexpr int kMaxChainPhases = 4;
+constexpr int kChainMaxN = 1024;
+constexpr int kChainSkip = 1 << 30;  // FrameRec.zcr flag bit: a non-finite frame keeps its phase-1 mel sums
 // dwords of one lane's mel record for R bins per lane (R weights, R slot bytes, R keep bytes,
 // 8 bytes of scan keeps and slots), padded to whole 16-byte loads
 __host__ __device__ constexpr int mel_rec_words(int R) { return (R + 2 * ((R + 3) / 4) + 2 + 3) / 4 * 4; }
@@ -26,6 +31,9 @@ struct DevTables {
   const uint32_t* mel_rec;   // 64 per-lane records of the mel segment tables (plan.cpp mel_lane_tables)
   const int* mel_bins;       // nfilt + 2 filter edges (mfcc.js:15-38), for the non-finite-frame path
   const float* dct;          // ncoef * nfilt, dct[c + j*ncoef] (mfcc.js:67-83)
+  // MGX_FLAG_MFCC_REFERENCE at N <= 1024 (plan.cpp chain_schedule, kernels.hip mel_chains):
+  const uint2* chain_lane;   // per phase and lane: (first bin | frame << 12 | band << 16 | valid << 31, weight offset)
+  const double* chain_w;     // per band, the weights of its chain steps (zero-padded to its phase's length)
 };
 
 struct KernelArgs {
@@ -53,6 +61,8 @@ struct KernelArgs {
   int mfcc_reference;    // MGX_FLAG_MFCC_REFERENCE: mel sums, log and DCT in the reference's order (SUB kernel)
   int mel_zero;          // some mel segment [b_m, b_{m+1}) is empty: the scan's slots are zeroed first
   int wg_ranks;          // workgroups per CU when the grid is the resident one (else 1): their work shares
+  int chain_nph;         // phases of the mel chain schedule (0: the segmented scan)
+  int chain_len[kMaxChainPhases];  // steps of each phase (multiples of 8)
 };
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.
@@ -77,8 +87,8 @@ struct UnpackArgs {
   int nseg;
 };
 hipError_t launch_unpack(const UnpackArgs& a, hipStream_t stream);
-size_t extract_lds_bytes(int n, int ncoef, int nfilt);
+size_t extract_lds_bytes(int n, int ncoef, int nfilt, bool chain);
 int frames_per_batch(int n);
-int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt);  // resident workgroups per CU
+int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt, bool chain);  // resident workgroups per CU
 
 }  // namespace mgx

@@ -285,6 +285,62 @@ void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& 
   }
 }
 
+// MGX_FLAG_MFCC_REFERENCE at N <= 1024: the mel band sums of mfcc.js:53-62 in the reference's
+// own order, as serial chains (kernels.hip mel_chains). Band j's chain walks its bins
+// [b_j, b_{j+2}) (clamped to the reference's j < N/2) in ascending order with the weights of
+// mfcc.js:43-50 -- (k - b_j) / (b_{j+1} - b_j) rising, (b_{j+2} - k) / (b_{j+2} - b_{j+1}) falling,
+// IEEE double quotients as JavaScript forms them -- and the float32 accumulator (every other bin
+// adds an exact +0 in the reference for a finite spectrum). A wave batch has 4 frames x nf such
+// chains; sorted by length they fill phases of 64 lanes (16 bands x the 4 frames: a band's 4
+// chains share a phase, its length the longest chain of the phase rounded up to 8 steps). A
+// lane reads Lp consecutive bins from its first bin, so a chain that would run past N/2 starts
+// earlier instead, with leading zero weights (a zero weight times a finite power adds +0).
+// Lanes without a chain read a table of zeros and store nothing; a band without bins (low bands
+// of many-band plans) has a chain of zero weights, so its energy is the reference's 0.
+//   lane record: (first bin | frame << 12 | band << 16 | 1 << 31, offset of the band's weights)
+struct ChainSched {
+  int nph = 0;
+  int len[mgx::kMaxChainPhases] = {0, 0, 0, 0};
+  std::vector<uint32_t> lane;  // 2 dwords per (phase, lane)
+  std::vector<double> w;
+};
+void chain_schedule(const int32_t* b, int nf, int L, ChainSched& cs) {
+  constexpr int F = 4;  // frames per wave batch (kernels.hip Geo::FPW)
+  std::vector<int> lo(nf), len(nf);
+  std::vector<int> order;
+  for (int j = 0; j < nf; ++j) {
+    lo[j] = std::min<int>(b[j], L);
+    len[j] = std::max(0, std::min<int>(b[j + 2], L) - lo[j]);
+    order.push_back(j);  // (an empty band too: its chain of zero weights stores the reference's 0)
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return len[x] > len[y]; });
+  const int per = 64 / F;  // bands per phase
+  cs.nph = ((int)order.size() + per - 1) / per;
+  cs.lane.assign((size_t)mgx::kMaxChainPhases * 128, 0u);
+  cs.w.assign((size_t)L, 0.0);  // [0, L): the zero table of idle lanes
+  for (int ph = 0; ph < cs.nph; ++ph) {
+    const int first = ph * per, last = std::min((int)order.size(), first + per);
+    const int lp = std::min(L, (len[order[first]] + 7) / 8 * 8);
+    cs.len[ph] = lp;
+    for (int i = first; i < last; ++i) {
+      const int j = order[i];
+      const int s0 = std::min(lo[j], L - lp), off = (int)cs.w.size();
+      for (int s = 0; s < lp; ++s) {
+        const int k = s0 + s;
+        double w = 0.0;
+        if (k >= b[j] && k < b[j + 1] && k < L) w = (double)(k - b[j]) / (double)(b[j + 1] - b[j]);
+        else if (k >= b[j + 1] && k < b[j + 2] && k < L) w = (double)(b[j + 2] - k) / (double)(b[j + 2] - b[j + 1]);
+        cs.w.push_back(w);
+      }
+      for (int f = 0; f < F; ++f) {
+        const int ln = (i - first) * F + f;
+        cs.lane[(size_t)ph * 128 + 2 * ln] = (uint32_t)s0 | (uint32_t)f << 12 | (uint32_t)j << 16 | 1u << 31;
+        cs.lane[(size_t)ph * 128 + 2 * ln + 1] = (uint32_t)off;
+      }
+    }
+  }
+}
+
 int validate(const mgx_plan_desc* d) {
   if (!d) return fail(MGX_E_INVALID_ARGUMENT, "plan descriptor is NULL");
   if (d->struct_size != sizeof(mgx_plan_desc))
@@ -324,6 +380,8 @@ struct mgx_plan {
   int grid_cap = 1;
   int cus = 0;  // compute units of the plan's device
   int mel_zero = 1;  // some mel segment is empty (kernels.hip mel_energies)
+  int chain_nph = 0;  // MGX_FLAG_MFCC_REFERENCE at N <= 1024: phases of the mel chains (chain_schedule)
+  int chain_len[mgx::kMaxChainPhases] = {0, 0, 0, 0};
   // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
   float* s_frames[2] = {nullptr, nullptr};
   unsigned char* s_out[2] = {nullptr, nullptr};
@@ -441,6 +499,10 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   mel_segments(bins.data(), nf, L, mwud, mseg);
   std::vector<uint32_t> mrec;
   mel_lane_tables(mseg, mwud, nf, L, mrec);
+  const bool chain = (d->flags & MGX_FLAG_MFCC_REFERENCE) && d->mode == MGX_MODE_PER_BUFFER_FFT &&
+                     d->precision == MGX_PRECISION_FAITHFUL && n <= mgx::kChainMaxN;
+  ChainSched cs;
+  if (chain) chain_schedule(bins.data(), nf, L, cs);
 
   auto* p = new mgx_plan();
   p->d = *d;
@@ -458,7 +520,9 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->nyq = d->sample_rate / (2.0 * (L - 1));  // spectralRolloff.js:4
   for (int i = 15; i < mgx::kBark; ++i) p->sharp_tail += 0.066 * exp(0.171 * (i + 1));  // perceptualSharpness.js:10
   // persistent grid: exactly the workgroups that are resident at once
-  p->grid_cap = prop.multiProcessorCount * std::max(1, mgx::extract_blocks_per_cu(n, (int)d->precision, (int)d->mode, (int)d->num_mfcc_coeffs, (int)d->num_mel_bands));
+  p->grid_cap = prop.multiProcessorCount * std::max(1, mgx::extract_blocks_per_cu(n, (int)d->precision, (int)d->mode, (int)d->num_mfcc_coeffs, (int)d->num_mel_bands, chain));
+  p->chain_nph = cs.nph;
+  for (int i = 0; i < mgx::kMaxChainPhases; ++i) p->chain_len[i] = cs.len[i];
   p->cus = prop.multiProcessorCount;
   // (tuning knob: MGX_GRID_CAP overrides the persistent grid's size; MGX_GRID_CAP=print reports it)
   if (const char* gc = getenv("MGX_GRID_CAP")) {
@@ -471,7 +535,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
                o_twf = carve<float>(off, twf.size()), o_twm = carve<double>(off, twm.size()),
                o_kl = carve<int>(off, L),
                o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<uint32_t>(off, mrec.size()), o_dct = carve<float>(off, dct.size()),
-               o_mb = carve<int32_t>(off, bins.size());
+               o_mb = carve<int32_t>(off, bins.size()), o_cl = carve<uint32_t>(off, cs.lane.size()),
+               o_cw = carve<double>(off, cs.w.size());
   std::vector<unsigned char> host(off, 0);
   auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) memcpy(host.data() + at, src, bytes); };
   put(o_win, d->window == MGX_WINDOW_HAMMING ? ham.data() : han.data(), n * sizeof(float));
@@ -483,6 +548,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   put(o_mw, mrec.data(), mrec.size() * sizeof(uint32_t));
   put(o_mb, bins.data(), bins.size() * sizeof(int32_t));
   put(o_dct, dct.data(), dct.size() * sizeof(float));
+  put(o_cl, cs.lane.data(), cs.lane.size() * sizeof(uint32_t));
+  put(o_cw, cs.w.data(), cs.w.size() * sizeof(double));
   e = hipMalloc(reinterpret_cast<void**>(&p->dev), off);
   if (e != hipSuccess) { delete p; return hip_fail(e, "hipMalloc(plan tables)"); }
   e = hipMemcpy(p->dev, host.data(), off, hipMemcpyHostToDevice);
@@ -497,6 +564,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->t.mel_rec = reinterpret_cast<const uint32_t*>(b + o_mw);
   p->t.mel_bins = reinterpret_cast<const int*>(b + o_mb);
   p->t.dct = reinterpret_cast<const float*>(b + o_dct);
+  p->t.chain_lane = reinterpret_cast<const uint2*>(b + o_cl);
+  p->t.chain_w = reinterpret_cast<const double*>(b + o_cw);
   *out = p;
   return MGX_OK;
 }
@@ -549,6 +618,8 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.dct_sequential = (p->d.flags & MGX_FLAG_DCT_SEQUENTIAL) ? 1 : 0;
   a.mfcc_reference = (p->d.flags & MGX_FLAG_MFCC_REFERENCE) ? 1 : 0;
   a.mel_zero = p->mel_zero;
+  a.chain_nph = p->chain_nph;
+  for (int i = 0; i < mgx::kMaxChainPhases; ++i) a.chain_len[i] = p->chain_len[i];
   bool spec = o->loudness_specific || o->mfcc || o->amplitude_spectrum || o->power_spectrum || o->complex_real;
   for (int i = MGX_SPECTRAL_CENTROID; i < MGX_NUM_SCALARS; ++i) spec = spec || o->scalars[i];
   a.need_spectrum = spec;

@@ -12,7 +12,7 @@ import sys
 def main(path, pat=""):
     txt = open(path).read()
     for part in re.split(r"\n(?=_ZN3mgx\S*:)", txt):
-        m = re.match(r"(_ZN3mgx\S*extract_kernelILi(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)\S*):", part)
+        m = re.match(r"(_ZN3mgx\S*extract_kernelILi(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)\S*):", part)
         if not m or pat not in m.group(1):
             continue
         depth = 0
@@ -25,7 +25,7 @@ def main(path, pat=""):
             if op:
                 k = ("st" if "store" in op.group(1) else "ld", depth)
                 hist[k] = hist.get(k, 0) + 1
-        tag = "N=%s faith=%s lit=%s sub=%s light=%s notime=%s" % m.group(2, 3, 4, 5, 6, 7)
+        tag = "N=%s faith=%s lit=%s sub=%s light=%s notime=%s chain=%s" % m.group(2, 3, 4, 5, 6, 7, 8)
         print(tag, " ".join("%s@d%d:%d" % (k[0], k[1], v) for k, v in sorted(hist.items())) or "no scratch")
 
 
