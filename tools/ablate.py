@@ -43,10 +43,9 @@ PATCHES = {
     "no_prefix": [("  const bool need_prefix = LIGHT ? false : SUB ? (bool)ap->need_prefix : true;",
                    "  const bool need_prefix = opaque(0);")],
     # MGX_FLAG_MFCC_REFERENCE (CHAIN kernels): the chains skipped (the occupancy / LDS-layout /
-    # power-row cost alone), or their weights from registers instead of the plan table
+    # power-row cost alone)
     "chain_none": [("        mel_chains<N>(q, opaque(lane), rows, reinterpret_cast<const float*>(buf), recs);",
                     "        if (opaque(0)) mel_chains<N>(q, opaque(lane), rows, reinterpret_cast<const float*>(buf), recs);")],
-    "chain_noload": [("        w[u] = wp[s + u];", "        w[u] = 0.5 + 0.001 * (s + u);")],
     "no_mel": [("  } else if (ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && ap->need_mfcc) {\n    mel_energies")],
 }
 

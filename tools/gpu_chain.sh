@@ -12,3 +12,6 @@ MGX_GRID_CAP=print timeout -k 10 300 python tools/mfcc_cost.py --n 1024 512 256 
 cat $O/cost_all.log | grep -v amdgpu.ids
 timeout -k 10 300 python tools/mfcc_cost.py --n 1024 512 --features c4 > $O/cost_c4.log 2>&1 || { tail -20 $O/cost_c4.log; exit 1; }
 grep -v amdgpu.ids $O/cost_c4.log
+echo "[chain] ablation: the chains skipped"
+MEYDA_AMD_LIB=$R/abl/libabl_chain_none.so timeout -k 10 300 python tools/mfcc_cost.py --n 1024 512 --rounds 5 > $O/cost_none.log 2>&1 || { tail -20 $O/cost_none.log; exit 1; }
+grep -v amdgpu.ids $O/cost_none.log
