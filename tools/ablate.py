@@ -14,7 +14,7 @@ SRC = os.path.join(ROOT, "meyda_amd", "csrc")
 
 # name -> list of (anchor, replacement); opaque(0) keeps the skipped code compiled but never run
 PATCHES = {
-    "no_phase2": [("    MGX_MARK(phase2_start);\n    prio_hi<4>();\n    {", "    MGX_MARK(phase2_start);\n    prio_hi<4>();\n    if (opaque(0)) {\n    {"),
+    "no_phase2": [("    MGX_MARK(phase2_start);\n    prio_hi<4>();\n", "    MGX_MARK(phase2_start);\n    prio_hi<4>();\n    if (opaque(0)) {\n"),
                   ("    prio_lo<4>();\n    MGX_MARK(phase2_end);", "    }\n    prio_lo<4>();\n    MGX_MARK(phase2_end);")],
     "no_loud2": [("if (!LIGHT && q->need_spectrum && q->need_loudness) {", "if (opaque(0) && !LIGHT && q->need_spectrum && q->need_loudness) {")],
     "no_ln": [("if (q->need_spectrum && q->need_mfcc) {\n        // mfcc.js:64",
@@ -46,7 +46,7 @@ PATCHES = {
     # power-row cost alone)
     "chain_none": [("        mel_chains<N>(q, opaque(lane), rows, reinterpret_cast<const float*>(buf), recs);",
                     "        if (opaque(0)) mel_chains<N>(q, opaque(lane), rows, reinterpret_cast<const float*>(buf), recs);")],
-    "no_mel": [("  } else if (ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && ap->need_mfcc) {\n    mel_energies")],
+    "no_mel": [("  } else if (!CHAIN && ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && !CHAIN && ap->need_mfcc) {\n    mel_energies")],
 }
 
 
