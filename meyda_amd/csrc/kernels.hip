@@ -219,6 +219,23 @@ struct TwLds {
   static constexpr int total() { return fw_off(Geo<N>::NPASS, 0); }
 };
 
+// The fast precision's LDS image (MGX_PRECISION_FAST, in the same LDS region): the float32
+// twiddles of the staged passes' stages are one contiguous range of the plan's twf table
+// (stage q at offset 2^q - 1, entries la | rp of both the mixed and the generic pairs).
+template <int N>
+struct TwLdsF {
+  using PG = PassGeo<N>;
+  static constexpr int first = (1 << PG::q0(1)) - 1;
+  static constexpr int qend() {
+    int q = PG::q0(1);
+    for (int p = 1; p < Geo<N>::NPASS; ++p)
+      if (TwLds<N>::pass_lds(p)) q = PG::q0(p) + PG::m(p);
+    return q;
+  }
+  static constexpr int count = (1 << qend()) - 1 - first;
+  static_assert(count * 8 <= TwLds<N>::total() * 16, "the float32 image fits the float64 one's LDS");
+};
+
 // Bank-padded layouts of the amplitude row (floats) and of its prefix sums (doubles) in
 // the slot buffer: lane l reads the row (ds_read2_b64) and writes the prefix
 // (ds_write2_b64) as R consecutive entries; both instructions serve 16 consecutive lanes
@@ -354,6 +371,30 @@ __device__ __forceinline__ void bfly_generic(float2& lo, float2& hi, GTw tw, GTw
   }
 }
 
+// The fast precision's generic and mixed pairs with the per-lane twiddle from LDS (TwLdsF).
+__device__ __forceinline__ void bfly_generic_f(float2& lo, float2& hi, float2 c) {
+  const float Ar = __builtin_fmaf(c.x, hi.x, -(c.y * hi.y));
+  const float Ai = __builtin_fmaf(c.x, hi.y, c.y * hi.x);
+  const float Lr = lo.x, Li = lo.y;
+  lo.x = __builtin_fmaf(kSf, Lr, Ar);
+  lo.y = __builtin_fmaf(kSf, Li, Ai);
+  hi.x = __builtin_fmaf(kSf, Lr, -Ar);
+  hi.y = __builtin_fmaf(-kSf, Li, Ai);
+}
+__device__ __forceinline__ void bfly_mixed_f(float2& lo, float2& hi, float2 c, float2 f, bool sp) {
+  const float Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
+  const float Ar = __builtin_fmaf(c.x, Rr, -(c.y * Ri));
+  const float Ai = __builtin_fmaf(c.x, Ri, c.y * Rr);
+  const float g0 = __builtin_fmaf(kSf, Lr, Ar), g1 = __builtin_fmaf(kSf, Li, Ai);
+  const float g2 = __builtin_fmaf(kSf, Lr, -Ar), g3 = __builtin_fmaf(-kSf, Li, Ai);
+  const float s0 = kSf * (Lr + Rr), s1 = kSf * (Lr - Rr);
+  const float s2 = __builtin_fmaf(kSf, Li, f.x * Ri), s3 = f.y * Ri;
+  lo.x = sp ? s0 : g0;
+  lo.y = sp ? s1 : g1;
+  hi.x = sp ? s2 : g2;
+  hi.y = sp ? s3 : g3;
+}
+
 // The faithful generic pair with its twiddle already in registers (TwLds).
 __device__ __forceinline__ void bfly_generic_c(float2& lo, float2& hi, double2 c) {
   const double Lr = lo.x, Li = lo.y, Rr = hi.x, Ri = hi.y;
@@ -475,6 +516,8 @@ template <int N, int P, int I, bool FAITH, bool TAME, bool TWL>
 __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw, GTwf twf, GTw twm,
                                           const double2* twl) {
   constexpr bool LT = FAITH && TAME && TWL && P > 0 && TwLds<N>::pass_lds(P);  // twiddles from the LDS image
+  constexpr bool LTF = !FAITH && TWL && P > 0 && TwLds<N>::pass_lds(P);        // the fast precision's (TwLdsF)
+  const float2* twlf = reinterpret_cast<const float2*>(twl);
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int q = PG::q0(P) + I;
@@ -506,9 +549,12 @@ __device__ __forceinline__ void run_stage(float2 (&v)[Geo<N>::R], int lp, GTw tw
           bfly_mixed_tame(v[r], v[hi], m, k, fw.x, sp);
         }
       }
+      else if constexpr (LTF) bfly_mixed_f(v[r], v[hi], twlf[mask - TwLdsF<N>::first + la], ld_twf_u(twf, fidx), la == 0);
       else bfly_mixed<FAITH>(v[r], v[hi], tw, twf, mask + la, fidx, la == 0);
     } else if constexpr (LT) {
       bfly_generic_c(v[r], v[hi], twl[TwLds<N>::off(P, I, true) + ((la | rp) - (1 << TwLds<N>::nl(P)))]);
+    } else if constexpr (LTF) {
+      bfly_generic_f(v[r], v[hi], twlf[mask - TwLdsF<N>::first + (la | rp)]);
     } else {
       bfly_generic<FAITH>(v[r], v[hi], tw, twf, mask + (la | rp));
     }
@@ -1618,6 +1664,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N
   }
   if constexpr (KGeo<N, CHAIN>::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
     stage_twiddles<N, 1, 0>(reinterpret_cast<double2*>(smem + LY::twl_off), gbl(ap->t.tw), gbl(ap->t.twm));
+  } else if constexpr (KGeo<N, CHAIN>::TW_LDS && !FAITH && !LITERAL) {  // the fast precision's (TwLdsF)
+    float2* d = reinterpret_cast<float2*>(smem + LY::twl_off);
+    const GTwf src = gbl(ap->t.twf);
+    for (int i = threadIdx.x; i < TwLdsF<N>::count; i += kThreads) d[i] = ld_twf(src, TwLdsF<N>::first + i);
   }
   if (ap->need_spectrum && ap->need_mfcc) {
     const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
