@@ -3,7 +3,7 @@
 patched copy of the kernel in which one part's work is skipped (results are WRONG: for
 timing only, with MEYDA_AMD_LIB pointing at the variant). Each patch is anchored on text
 of meyda_amd/csrc/kernels.hip and fails loudly if the anchor moved.
-usage: ablate.py NAME [NAME ...]   (names: see PATCHES; 'all' builds every one)"""
+usage: ablate.py NAME [NAME ...]   (names: see PATCHES, or a+b+... for several at once; 'all' builds every one)"""
 import os
 import subprocess
 import sys
@@ -46,13 +46,26 @@ PATCHES = {
     # power-row cost alone)
     "chain_none": [("        mel_chains<N>(q, opaque(lane), rows, reinterpret_cast<const float*>(buf), recs);",
                     "        if (opaque(0)) mel_chains<N>(q, opaque(lane), rows, reinterpret_cast<const float*>(buf), recs);")],
+    # the FFT passes after pass 0 skipped (the exchanges too): what the f64 butterflies cost
+    "no_passes": [("      if (tame) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);",
+                   "      if (opaque(0)) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);"),
+                  ("      else run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);",
+                   "      else if (opaque(0)) run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);")],
+    # the whole FFT after stage 0 skipped
+    "no_fft": [("      run_stages<N, 0, 0, FAITH, false, TWL>(v, lpf[0], tw, twf, twm, twl);",
+                "      if (opaque(0)) run_stages<N, 0, 0, FAITH, false, TWL>(v, lpf[0], tw, twf, twm, twl);"),
+               ("      if (tame) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);",
+                "      if (opaque(0)) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);"),
+               ("      else run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);",
+                "      else if (opaque(0)) run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);")],
     "no_mel": [("  } else if (!CHAIN && ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && !CHAIN && ap->need_mfcc) {\n    mel_energies")],
 }
 
 
 def build(name, flags=()):
     src = open(os.path.join(SRC, "kernels.hip")).read()
-    for old, new in PATCHES[name]:
+    # "a+b": the patches of a, then those of b (cumulative ablations)
+    for old, new in [pt for part in name.split("+") for pt in PATCHES[part]]:
         if src.count(old) != 1:
             raise SystemExit("%s: anchor found %d times: %r" % (name, src.count(old), old[:60]))
         src = src.replace(old, new)
@@ -61,7 +74,7 @@ def build(name, flags=()):
     tmp = tempfile.NamedTemporaryFile("w", suffix=".hip", dir=os.path.join(ROOT, "abl"), prefix=".abl_", delete=False)
     tmp.write(src)
     tmp.close()
-    out = os.path.join(ROOT, "abl", "libabl_%s.so" % name)
+    out = os.path.join(ROOT, "abl", "libabl_%s.so" % name.replace("+", "_"))
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
            "-mllvm", "-disable-machine-licm", "-I", SRC, *flags, "-shared", "-o", out, "-x", "hip", tmp.name,
            os.path.join(SRC, "plan.cpp"), os.path.join(SRC, "group.cpp"), "-ldl"]
