@@ -134,17 +134,6 @@ struct Geo {
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
 };
 
-// The kernel instances with the mel sums as chains in the reference's order (CHAIN:
-// MGX_FLAG_MFCC_REFERENCE at N <= 1024, mel_chains) hold the batch's power rows in LDS (3 rows
-// per wave; the 4th in the slot buffer): at N = 1024 the tame passes' twiddles leave the LDS
-// for them and the workgroups per CU go from 4 to 3 (so the register bound from 128 to 168).
-template <int N, bool CHAIN>
-struct KGeo {
-  static constexpr bool TW_LDS = Geo<N>::TW_LDS && !(CHAIN && N == 1024);
-  static constexpr int WPE = !CHAIN ? Geo<N>::WPE : N <= 256 ? 5 : N <= 512 ? 4 : 3;
-  static constexpr int ROWS = CHAIN ? 3 : 0;  // power rows per wave in LDS of their own
-};
-
 // Location bits of pass p: register bits [0, m) drive location bits [q0, q0+m); the
 // six lane bits take the lowest remaining location bits; leftover register bits
 // take the rest. Pass 0 is fixed by the load: location = rev6(lane)*R + r.
@@ -771,7 +760,7 @@ __device__ __forceinline__ void put_scalar(KArgs* a, int i, uint64_t f, double v
   if (a->out.scalars[i]) gbl(static_cast<T*>(a->out.scalars[i]))[f] = (T)v;
 }
 
-template <int N, bool CHAIN = false>
+template <int N>
 struct Lds {
   using G = Geo<N>;
   // One slot buffer per wave: FFT exchanges, then the frame's amplitude row, its prefix
@@ -794,13 +783,10 @@ struct Lds {
   static constexpr size_t kc_bytes = 16 * 8 + 32 * 4;
   // The tame passes' per-lane twiddles (Geo<N>::TW_LDS, TwLds), staged once per workgroup.
   static constexpr size_t twl_off = kc_off + kc_bytes;
-  static constexpr size_t twl_bytes = KGeo<N, CHAIN>::TW_LDS ? (size_t)TwLds<N>::total() * 16 : 0;
+  static constexpr size_t twl_bytes = Geo<N>::TW_LDS ? (size_t)TwLds<N>::total() * 16 : 0;
   static_assert(twl_off % 16 == 0, "double2 alignment");
-  // CHAIN: the power rows of the first three frames of each wave's batch (mel_chains).
-  static constexpr size_t rows_off = twl_off + twl_bytes;
-  static constexpr size_t rows_bytes = (size_t)4 * KGeo<N, CHAIN>::ROWS * G::L * 4;
   // The DCT table (mfcc.js:67-83), staged once per workgroup, sized per plan.
-  static constexpr size_t dct_off = rows_off + rows_bytes;
+  static constexpr size_t dct_off = twl_off + twl_bytes;
   static size_t bytes(int ncoef, int nfilt) { return dct_off + (size_t)ncoef * ((nfilt + 7) & ~7) * 4; }
 };
 
@@ -908,7 +894,7 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
 // as the reference does (see frame_phase1). The amplitude row is rewritten to the slot buffer.
 template <int N>
 __device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av)[Geo<N>::R], int lane,
-                                                               float2* buf, FrameRec& rec) {
+                                                               float2* buf, FrameRec& rec, int lmo = 0) {
   constexpr int L = N / 2, R = Geo<N>::R;
   float* amp = reinterpret_cast<float*>(buf);
   wave_sync();  // prefix reads (band sums) are done
@@ -934,7 +920,7 @@ __device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av
         const float p = amp[k] * amp[k];
         e = (float)((double)e + w * (double)p);
       }
-      rec.lm[j] = e;
+      rec.lm[lmo + j] = e;
     }
   }
 }
@@ -990,40 +976,57 @@ __device__ __forceinline__ void mel_reference_order(KArgs* ap, const float (&av)
   }
 }
 
-// MGX_FLAG_MFCC_REFERENCE at N <= 1024 (the CHAIN kernels): the mel band energies of the wave's
-// batch in the reference's own order (mfcc.js:53-62), over the 4 power rows phase 1 left in LDS.
-// Each band of each frame is one serial chain: from its first bin in ascending order, the weight
-// (an IEEE double quotient, plan table) times the float32 power rounded to double, added to the
-// Float32Array element in double and stored back to float32 -- exactly the reference's
-// operations, so the sums are the reference's bits. The host schedule (plan.cpp chain_schedule)
-// puts 64 chains side by side per phase, a band's 4 frames in one phase, every lane of a phase
-// running its length; the critical path is the longest band (120 bins at N = 1024 with 26 bands),
-// shared by the batch's 4 frames. Per step: one LDS read, one (cached) weight load, and the
-// conversion, product, sum and the two roundings on the VALU.
+// MGX_FLAG_MFCC_REFERENCE at N <= 1024 (the CHAIN kernels): the mel band energies in the reference's
+// own order (mfcc.js:53-62), over the power rows phase 1 left in the wave's ring in device memory
+// (KernelArgs::chain_rows). Each band of each frame is one serial chain: from its first bin in
+// ascending order, the weight (an IEEE double quotient, plan table) times the float32 power rounded
+// to double, added to the Float32Array element in double and stored back to float32 -- exactly the
+// reference's operations, so the sums are the reference's bits. The host schedule (plan.cpp
+// chain_schedule) puts 64 chains side by side per phase, a band's F frames in one phase, every lane
+// of a phase running its length from a 4-aligned first bin (16-byte row loads).
+//   F = 8 (KernelArgs::chain_pair, nfilt <= 31): the chains of two consecutive batches of the wave
+//     run together, in the second batch's phase 2 (ring slots 0..3 the first batch, 4..7 the
+//     second): the longest band (120 bins at N = 1024, 26 bands) is then shared by 8 frames instead
+//     of 4, and the lanes are busy for most of its length. The first batch's energies go to the
+//     upper half of its records' lm (lm[32 + band]); lm[31] / lm[63] hold the frame's non-finite
+//     flag (its energies then come from nonfinite_frame_sums). have_cur = false (the wave's last
+//     batch was the first of a pair) stores only the first batch's.
+//   F = 4 (more bands): the batch's chains in its own phase 2, slots 0..3, the non-finite flag a bit
+//     of the record's zcr count.
+// Per step: the conversion, product, sum and the two roundings on the VALU; per 8 steps two 16-byte
+// row loads and the 8 weights.
 template <int N>
-__device__ __forceinline__ void mel_chains(KArgs* q, int lane, const float* rows, const float* last, FrameRec* recs) {
+__device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec* recs, bool pair, bool have_cur) {
   constexpr int L = N / 2;
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) f32x4* GF4;
   const auto cl = gbl(reinterpret_cast<const uint32_t*>(q->t.chain_lane));
   const auto cw = gbl(q->t.chain_w);
   for (int ph = 0; ph < q->chain_nph; ++ph) {
     const uint32_t rx = cl[2 * (ph * 64 + lane)], ry = cl[2 * (ph * 64 + lane) + 1];
-    const int s0 = (int)(rx & 0xFFFu), fr = (int)((rx >> 12) & 3u), band = (int)((rx >> 16) & 0x7Fu);
-    const float* pr = (fr < Geo<N>::FPW - 1 ? rows + fr * L : last) + s0;
+    const int s0 = (int)(rx & 0xFFFu), fr = (int)((rx >> 12) & 7u), band = (int)((rx >> 16) & 0x7Fu);
+    const GF4 pr = (GF4)(ring + fr * L + s0);  // s0 is a multiple of 4 (chain_schedule)
     const auto wp = cw + ry;
     const int len = q->chain_len[ph];
     double acc = 0.0;  // the Float32Array element, held exactly in double
     for (int s = 0; s < len; s += 8) {
-      float p[8];
+      const f32x4 p0 = pr[s / 4], p1 = pr[s / 4 + 1];
+      const float p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
       double w[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        p[u] = pr[s + u];
-        w[u] = wp[s + u];
-      }
+      for (int u = 0; u < 8; ++u) w[u] = wp[s + u];
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc = (double)(float)(acc + w[u] * (double)p[u]);  // two roundings, the float32 store
     }
-    if ((int)rx < 0 && !(recs[fr].zcr & kChainSkip)) recs[fr].lm[band] = (float)acc;
+    if ((int)rx < 0) {
+      if (!pair) {
+        if (!(recs[fr].zcr & kChainSkip)) recs[fr].lm[band] = (float)acc;
+      } else {
+        FrameRec& r = recs[fr & 3];
+        const int lmo = fr < 4 ? 32 : 0;  // the pair's first batch: the upper half
+        if ((fr < 4 || have_cur) && r.lm[lmo + 31] == 0.0f) r.lm[lmo + band] = (float)acc;
+      }
+    }
   }
 }
 
@@ -1034,11 +1037,11 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
                                              const int* klim, float (&xn)[Geo<N>::PREFETCH ? Geo<N>::CH : 1],
                                              GF next, const double2* twl, const float (&wreg)[Geo<N>::CH],
-                                             uint32_t blim, float* rows) {
+                                             uint32_t blim, float* rows, int it) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
-  constexpr bool TWL = KGeo<N, CHAIN>::TW_LDS;
+  constexpr bool TWL = Geo<N>::TW_LDS;
   float* amp = reinterpret_cast<float*>(buf);  // the frame's amplitude row, once the FFT is done
   double* pbuf = reinterpret_cast<double*>(buf);
 
@@ -1456,22 +1459,28 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   MGX_MARK(bands_done);
   const bool nonfinite = light ? light_nonfinite : !(total < __builtin_huge_val());
   if (nonfinite) {
-    nonfinite_frame_sums<N>(ap, av, lane, buf, rec);
+    // (CHAIN with paired batches: the pair's first batch keeps its mel sums in the upper half of lm)
+    nonfinite_frame_sums<N>(ap, av, lane, buf, rec, CHAIN && ap->chain_pair && !(it & 1) ? 32 : 0);
   } else if (!CHAIN && SUB && ap->need_mfcc && ap->mfcc_reference) {  // (N = 2048 only; the all-feature kernel never has the flag)
     mel_reference_order<N>(ap, av, lane, buf, rec);
   } else if (!CHAIN && ap->need_mfcc) {
     mel_energies<N>(ap, av, lane, buf, rec, mt);
   }
   if constexpr (CHAIN) {
-    // the frame's power row (powerSpectrum.js) for the batch's mel chains in phase 2: the first
-    // three frames of the batch in rows of their own, the last in the slot buffer; a non-finite
-    // frame keeps the mel sums nonfinite_frame_sums formed (kChainSkip, a bit of its zcr count)
+    // the frame's power row (powerSpectrum.js) for the mel chains in phase 2 (mel_chains): ring slot
+    // fb, or with paired batches 4 (it & 1) + fb; a non-finite frame keeps the mel sums
+    // nonfinite_frame_sums formed (its flag: lm[31] of its half, or a bit of its zcr count)
     if (ap->need_mfcc) {
-      float* row = fb < Geo<N>::FPW - 1 ? rows + fb * L : amp;
-      wave_sync();  // the slot buffer's band-sum (and non-finite) reads are done
+      const bool pair = ap->chain_pair;
+      // (the wave's ring in device memory: R consecutive floats per lane)
+      auto row = gbl(rows) + ((pair ? 4 * (it & 1) : 0) + fb) * L;
 #pragma unroll
       for (int jj = 0; jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];
-      if (nonfinite && lane == 0) rec.zcr = rec.zcr | kChainSkip;
+      if (pair) {
+        if (lane == 0) rec.lm[(it & 1 ? 0 : 32) + 31] = nonfinite ? 1.0f : 0.0f;
+      } else if (nonfinite && lane == 0) {
+        rec.zcr = rec.zcr | kChainSkip;
+      }
     }
   }
   MGX_MARK(mel_done);
@@ -1609,6 +1618,71 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   return sc == MGX_RMS ? sqrt_d(v) : sc == MGX_PERCEPTUAL_SPREAD ? v * v : v;
 }
 
+// mfcc.js:64: Math.log of the batch's band energies (lm[lmo + band] of its FPW records), stored
+// to Float32Array; bands past nfilt (up to the DCT table's padded width) become 0. Two bands per
+// lane (a pair of adjacent floats: one LDS read and write each): the batch's 4 frames x 32 bands in
+// one pass.
+template <bool CHAIN, bool SUB>
+__device__ __forceinline__ void mfcc_log(KArgs* q, int l2, FrameRec* recs, int lmo) {
+  constexpr int FPW = 4;
+  const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
+  const bool ref_log = CHAIN || (SUB && q->mfcc_reference);  // the double Math.log, then float32
+  auto ln1 = [&](float v, int band) {
+    return band < nfilt ? (ref_log ? (float)log((double)v) : ln_f32(v)) : 0.0f;  // padding for dct_sum
+  };
+  for (int i = l2; i < FPW * (nfp / 2); i += 64) {
+    const int fb = i % FPW, band = 2 * (i / FPW);
+    f32x2* pp = reinterpret_cast<f32x2*>(&recs[fb].lm[lmo + band]);
+    const f32x2 v = *pp;
+    *pp = f32x2{ln1(v.x, band), ln1(v.y, band + 1)};
+  }
+}
+
+// mfcc.js:67-93: the DCT of the batch's log energies (lm[lmo + ...] of its FPW records), stored to
+// the mfcc rows of frames fbase .. fbase + FPW - 1.
+template <bool CHAIN, bool SUB>
+__device__ __forceinline__ void mfcc_dct(KArgs* q, int l2, FrameRec* recs, const float* dct_lds, int lmo, uint64_t fbase) {
+  constexpr int FPW = 4;
+  const int nc = q->ncoef, nfilt = q->nfilt;
+  if (q->dct_sequential || (SUB && !CHAIN && q->mfcc_reference)) {
+    // MGX_FLAG_DCT_SEQUENTIAL: VALU FMAs in the reference's sequential order, one lane per
+    // (coefficient, frame). (The matrix-core form below is the default: 0.5 % faster for the
+    // whole kernel and equal on every golden coefficient)
+    for (int i = l2; i < FPW * nc; i += 64) {
+      const int c = i / FPW, fb = i % FPW;
+      const uint64_t f = fbase + fb;
+      const double v = dct_sum(dct_lds, recs[fb].lm + lmo, c, nc, nfilt);
+      if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)div_by(v, nc, q->rcp_ncoef);
+    }
+    return;
+  }
+  // mfcc.js:85-93 on the FP64 matrix cores, v_mfma_f64_4x4x4_4b_f64: 4 blocks of a 4 x 4 x 4
+  // product per instruction. Block g holds coefficients 4g..4g+3 of a 16-coefficient tile against
+  // the batch's 4 frames; a step covers 4 bands. Lane layout (measured,
+  // tools/ubench/mfma_f64_4x4_layout.hip): A[i][k] of block g at lane 16k + 4g + i, B[k][j] at
+  // 16k + 4g + j, D[i][j] at 16i + 4g + j. So lane l loads DCT[c = l & 15][band n0 + (l >> 4)] and
+  // lm[frame l & 3][band n0 + (l >> 4)], and ends with coefficient 4 ((l >> 2) & 3) + (l >> 4) of
+  // frame l & 3. The products of two floats are exact in double, as in the reference; only the f64
+  // summation order differs.
+  static_assert(FPW == 4, "one 4 x 4 block column per frame of the batch");
+  const int kk = l2 >> 4, fa = l2 & 3, nsteps = (nfilt + 3) >> 2;
+  const float* lmrow = recs[fa].lm + lmo;
+  for (int mt = 0; mt < nc; mt += 16) {
+    // (a tile row past the last coefficient reads the last row again instead of a guarded zero:
+    // a row of A only feeds its own coefficient's outputs, never stored)
+    const int ca = min(mt + (l2 & 15), nc - 1);
+    double acc = 0.0;
+    for (int st = 0; st < nsteps; ++st) {
+      const int n = 4 * st + kk;  // < nfilt rounded up to 8: the tables are zero-padded
+      const float av = dct_lds[ca + n * nc];
+      acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)av, (double)lmrow[n], acc, 0, 0, 0);
+    }
+    const int c = mt + 4 * ((l2 >> 2) & 3) + kk;
+    const uint64_t f = fbase + fa;
+    if (c < nc && f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)div_by(acc, nc, q->rcp_ncoef);
+  }
+}
+
 // Copy of the TwLds image from the plan tables, once per workgroup (before its LDS barrier).
 template <int N, int P, int I>
 __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
@@ -1635,10 +1709,10 @@ __device__ unsigned long long g_wave_times[65536 * 4];
 #endif
 
 template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N, CHAIN>::WPE))) void extract_kernel(KernelArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
-  using LY = Lds<N, CHAIN>;
+  using LY = Lds<N>;
   constexpr int R = G::R, CH = G::CH, FPW = G::FPW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* slot_all = reinterpret_cast<float2*>(smem + LY::slot_off);
@@ -1649,7 +1723,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float2* buf = slot_all + wave * G::SLOT_PHYS;
   FrameRec* recs = reinterpret_cast<FrameRec*>(smem + LY::rec_off) + wave * FPW;  // this wave's records
-  float* rows = reinterpret_cast<float*>(smem + LY::rows_off) + wave * KGeo<N, CHAIN>::ROWS * G::L;  // CHAIN: power rows
+  // CHAIN: the wave's ring of power rows in device memory (2 FPW rows: paired batches, mel_chains)
+  float* rows = CHAIN ? uniform_ptr(args_ptr()->chain_rows + ((uint64_t)blockIdx.x * 4 + wave) * (uint64_t)(2 * FPW * G::L))
+                      : nullptr;
   KArgs* ap = args_ptr();
 #if MGX_WAVE_TIMES
   const unsigned long long wt0 = wall_clock64();
@@ -1662,9 +1738,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N
     if (threadIdx.x < MGX_NUM_SCALARS) kptr[threadIdx.x] = ap->out.scalars[threadIdx.x];
     if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = gbl(ap->t.bblim)[threadIdx.x - 64];
   }
-  if constexpr (KGeo<N, CHAIN>::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
+  if constexpr (Geo<N>::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
     stage_twiddles<N, 1, 0>(reinterpret_cast<double2*>(smem + LY::twl_off), gbl(ap->t.tw), gbl(ap->t.twm));
-  } else if constexpr (KGeo<N, CHAIN>::TW_LDS && !FAITH && !LITERAL) {  // the fast precision's (TwLdsF)
+  } else if constexpr (Geo<N>::TW_LDS && !FAITH && !LITERAL) {  // the fast precision's (TwLdsF)
     float2* d = reinterpret_cast<float2*>(smem + LY::twl_off);
     const GTwf src = gbl(ap->t.twf);
     for (int i = threadIdx.x; i < TwLdsF<N>::count; i += kThreads) d[i] = ld_twf(src, TwLdsF<N>::first + i);
@@ -1777,7 +1853,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N
   float xn[G::PREFETCH ? CH : 1];
   if constexpr (G::PREFETCH) load(xn, b0, 0);
 
-  for (uint64_t b = b0; b < bend; b += wstride) {
+  int it = 0;  // the wave's batch count (CHAIN with paired batches: the pair's second when odd)
+  for (uint64_t b = b0; b < bend; b += wstride, ++it) {
     const uint64_t f0 = b * FPW;
     // ------------------------------------------------------------- phase 1
     for (int j = 0; j < FPW; ++j) {
@@ -1798,7 +1875,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N
       }
       frame_phase1<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
                                       reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
-                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim, rows);
+                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim, rows, it);
     }
     wave_sync();
 
@@ -1807,10 +1884,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N
     // hoisted out of the batch loop (it would stay live across the FFT).
     MGX_MARK(phase2_start);
     prio_hi<4>();
+    // CHAIN: the mel chains, then the log and the DCT, every batch -- or with paired batches
+    // (chain_pair) every second batch of the wave, for the pair (its first batch's energies in the
+    // upper half of lm)
+    bool mfcc_now = false;
     if constexpr (CHAIN) {
       KArgs* q = args_ptr();
-      if (q->need_spectrum && q->need_mfcc) {
-        mel_chains<N>(q, opaque(lane), rows, reinterpret_cast<const float*>(buf), recs);
+      mfcc_now = q->need_spectrum && q->need_mfcc && (!q->chain_pair || (it & 1));
+      if (mfcc_now) {
+        // the rows' stores (every lane's) complete before any lane reads them: the ring is this
+        // wave's alone and the CU's L1 is coherent for its own waves (workgroup scope)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        mel_chains<N>(q, opaque(lane), gbl(rows), recs, q->chain_pair, true);
         wave_sync();  // the band energies are in the records: the log step reads them
       }
     }
@@ -1856,21 +1942,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N
         }
       }
       MGX_MARK(loud2_done);
-      if (q->need_spectrum && q->need_mfcc) {
-        // mfcc.js:64 Math.log of the band energies, stored to Float32Array
-        const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
-        const bool ref_log = CHAIN || (SUB && q->mfcc_reference);  // the double Math.log, then float32
-        // two bands per lane (a pair of adjacent floats: one LDS read and write each): the
-        // batch's 4 frames x 32 bands in one pass
-        auto ln1 = [&](float v, int band) {
-          return band < nfilt ? (ref_log ? (float)log((double)v) : ln_f32(v)) : 0.0f;  // padding for dct_sum
-        };
-        for (int i = l2; i < FPW * (nfp / 2); i += 64) {
-          const int fb = i % FPW, band = 2 * (i / FPW);
-          f32x2* pp = reinterpret_cast<f32x2*>(&recs[fb].lm[band]);
-          const f32x2 v = *pp;
-          *pp = f32x2{ln1(v.x, band), ln1(v.y, band + 1)};
-        }
+      if (CHAIN ? mfcc_now : (q->need_spectrum && q->need_mfcc)) {
+        mfcc_log<CHAIN, SUB>(q, l2, recs, 0);
+        if (CHAIN && q->chain_pair) mfcc_log<CHAIN, SUB>(q, l2, recs, 32);  // the pair's first batch
       }
     }
     wave_sync();
@@ -1878,45 +1952,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N
       KArgs* q = args_ptr();
       const int l2 = opaque(lane);
       MGX_MARK(ln_done);
-      if (q->need_spectrum && q->need_mfcc) {
-        const int nc = q->ncoef, nfilt = q->nfilt;
-        if (q->dct_sequential || (SUB && !CHAIN && q->mfcc_reference)) {
-        // MGX_FLAG_DCT_SEQUENTIAL: VALU FMAs in the reference's sequential order, one lane per
-        // (coefficient, frame). (The matrix-core form below is the default: 0.5 % faster for the
-        // whole kernel and equal on every golden coefficient)
-        for (int i = l2; i < FPW * nc; i += 64) {
-          const int c = i / FPW, fb = i % FPW;
-          const uint64_t f = f0 + fb;
-          const double v = dct_sum(dct_lds, recs[fb].lm, c, nc, nfilt);
-          if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)div_by(v, nc, q->rcp_ncoef);
-        }
-        } else {
-        // mfcc.js:85-93 on the FP64 matrix cores, v_mfma_f64_4x4x4_4b_f64: 4 blocks of a
-        // 4 x 4 x 4 product per instruction. Block g holds coefficients 4g..4g+3 of a
-        // 16-coefficient tile against the batch's 4 frames; a step covers 4 bands. Lane layout
-        // (measured, tools/ubench/mfma_f64_4x4_layout.hip): A[i][k] of block g at lane
-        // 16k + 4g + i, B[k][j] at 16k + 4g + j, D[i][j] at 16i + 4g + j. So lane l loads
-        // DCT[c = l & 15][band n0 + (l >> 4)] and lm[frame l & 3][band n0 + (l >> 4)], and ends
-        // with coefficient 4 ((l >> 2) & 3) + (l >> 4) of frame l & 3. The products of two
-        // floats are exact in double, as in the reference; only the f64 summation order differs.
-        static_assert(FPW == 4, "one 4 x 4 block column per frame of the batch");
-        const int kk = l2 >> 4, fa = l2 & 3, nsteps = (nfilt + 3) >> 2;
-        const float* lmrow = recs[fa].lm;
-        for (int mt = 0; mt < nc; mt += 16) {
-          // (a tile row past the last coefficient reads the last row again instead of a
-          // guarded zero: a row of A only feeds its own coefficient's outputs, never stored)
-          const int ca = min(mt + (l2 & 15), nc - 1);
-          double acc = 0.0;
-          for (int st = 0; st < nsteps; ++st) {
-            const int n = 4 * st + kk;  // < nfilt rounded up to 8: the tables are zero-padded
-            const float av = dct_lds[ca + n * nc];
-            acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)av, (double)lmrow[n], acc, 0, 0, 0);
-          }
-          const int c = mt + 4 * ((l2 >> 2) & 3) + kk;
-          const uint64_t f = f0 + fa;
-          if (c < nc && f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)div_by(acc, nc, q->rcp_ncoef);
-        }
-        }
+      if (CHAIN ? mfcc_now : (q->need_spectrum && q->need_mfcc)) {
+        mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 0, f0);
+        if (CHAIN && q->chain_pair) mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 32, f0 - wstride * FPW);  // the pair's first batch
       }
       MGX_MARK(dct_done);
       // the scalar features: one lane per (feature, frame); the loudness total, perceptual
@@ -1934,6 +1972,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(KGeo<N
     prio_lo<4>();
     MGX_MARK(phase2_end);
     wave_sync();  // records and slot buffer are reused by the next batch
+  }
+  if constexpr (CHAIN) {
+    // paired batches: a wave whose last batch opened a pair finishes that batch's mfcc alone
+    KArgs* q = args_ptr();
+    if (q->need_spectrum && q->need_mfcc && q->chain_pair && (it & 1)) {
+      prio_hi<4>();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const int l2 = opaque(lane);
+      mel_chains<N>(q, l2, gbl(rows), recs, true, false);
+      wave_sync();
+      mfcc_log<CHAIN, SUB>(q, l2, recs, 32);
+      wave_sync();
+      mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 32, (b0 + (uint64_t)(it - 1) * wstride) * FPW);
+      prio_lo<4>();
+    }
   }
 #if MGX_WAVE_TIMES
   if (lane == 0 && blockIdx.x < 16384) {
@@ -2005,7 +2059,7 @@ __global__ void unpack_kernel(UnpackArgs a) {
 
 template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false, bool CHAIN = false>
 hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
-  const size_t lds = Lds<N, CHAIN>::bytes(a.ncoef, a.nfilt);
+  const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
   hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN>), dim3(grid), dim3(kThreads), lds, stream, a);
   return hipGetLastError();
 }
@@ -2014,7 +2068,7 @@ template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false,
 int occupancy_n(int ncoef, int nfilt) {
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN>, kThreads,
-                                                   Lds<N, CHAIN>::bytes(ncoef, nfilt)) != hipSuccess)
+                                                   Lds<N>::bytes(ncoef, nfilt)) != hipSuccess)
     return 0;
   return blocks;
 }
@@ -2075,9 +2129,9 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
 
 size_t extract_lds_bytes(int n, int ncoef, int nfilt, bool chain) {
   switch (n) {
-    case 256: return chain ? Lds<256, true>::bytes(ncoef, nfilt) : Lds<256>::bytes(ncoef, nfilt);
-    case 512: return chain ? Lds<512, true>::bytes(ncoef, nfilt) : Lds<512>::bytes(ncoef, nfilt);
-    case 1024: return chain ? Lds<1024, true>::bytes(ncoef, nfilt) : Lds<1024>::bytes(ncoef, nfilt);
+    case 256: return Lds<256>::bytes(ncoef, nfilt);
+    case 512: return Lds<512>::bytes(ncoef, nfilt);
+    case 1024: return Lds<1024>::bytes(ncoef, nfilt);
     case 2048: return Lds<2048>::bytes(ncoef, nfilt);
     default: return 0;
   }

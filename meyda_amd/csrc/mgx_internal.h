@@ -12,9 +12,10 @@ constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
 constexpr int kMelHead = kMaxMel + 2;  // mel scratch: segment sums [0, nfilt + 2), head partials from here
-// Mel band chains in the reference's own order (MGX_FLAG_MFCC_REFERENCE, N <= 1024): a wave
-// batch's 4 frames x nfilt chains, 64 per phase, so at most 4 phases.
+// Mel band chains in the reference's own order (MGX_FLAG_MFCC_REFERENCE, N <= 1024): F frames x
+// nfilt chains, 64 per phase (F = 8 for nfilt <= 31, else F = 4), so at most 4 phases.
 constexpr int kMaxChainPhases = 4;
+constexpr int kChainPairMaxMel = 31;  // paired batches keep two halves of FrameRec::lm (flag at 31)
 constexpr int kChainMaxN = 1024;
 constexpr int kChainSkip = 1 << 30;  // FrameRec.zcr flag bit: a non-finite frame keeps its phase-1 mel sums
 // dwords of one lane's mel record for R bins per lane (R weights, R slot bytes, R keep bytes,
@@ -63,6 +64,8 @@ struct KernelArgs {
   int wg_ranks;          // workgroups per CU when the grid is the resident one (else 1): their work shares
   int chain_nph;         // phases of the mel chain schedule (0: the segmented scan)
   int chain_len[kMaxChainPhases];  // steps of each phase (multiples of 8)
+  int chain_pair;        // the chains of two consecutive batches of a wave run together (8 frames, nfilt <= 31)
+  float* chain_rows;     // the chains' power rows: 2 FPW x N/2 floats per wave of the grid (kernels.hip mel_chains)
 };
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.

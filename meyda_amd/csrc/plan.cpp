@@ -290,11 +290,13 @@ void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& 
 // [b_j, b_{j+2}) (clamped to the reference's j < N/2) in ascending order with the weights of
 // mfcc.js:43-50 -- (k - b_j) / (b_{j+1} - b_j) rising, (b_{j+2} - k) / (b_{j+2} - b_{j+1}) falling,
 // IEEE double quotients as JavaScript forms them -- and the float32 accumulator (every other bin
-// adds an exact +0 in the reference for a finite spectrum). A wave batch has 4 frames x nf such
-// chains; sorted by length they fill phases of 64 lanes (16 bands x the 4 frames: a band's 4
-// chains share a phase, its length the longest chain of the phase rounded up to 8 steps). A
-// lane reads Lp consecutive bins from its first bin, so a chain that would run past N/2 starts
-// earlier instead, with leading zero weights (a zero weight times a finite power adds +0).
+// adds an exact +0 in the reference for a finite spectrum). F frames x nf such chains run together
+// (F = 8: two consecutive batches of a wave, when nf <= kChainPairMaxMel; else the batch's 4);
+// sorted by length they fill phases of 64 lanes (64 / F bands x the F frames: a band's chains
+// share a phase, its length the longest chain of the phase rounded up to 8 steps). A lane reads Lp
+// consecutive bins from its first bin, which is a multiple of 4 (16-byte row loads): a chain starts
+// at its first bin rounded down to 4, or earlier if it would run past N/2, with leading zero
+// weights (a zero weight times a finite power adds +0).
 // Lanes without a chain read a table of zeros and store nothing; a band without bins (low bands
 // of many-band plans) has a chain of zero weights, so its energy is the reference's 0.
 //   lane record: (first bin | frame << 12 | band << 16 | 1 << 31, offset of the band's weights)
@@ -304,13 +306,13 @@ struct ChainSched {
   std::vector<uint32_t> lane;  // 2 dwords per (phase, lane)
   std::vector<double> w;
 };
-void chain_schedule(const int32_t* b, int nf, int L, ChainSched& cs) {
-  constexpr int F = 4;  // frames per wave batch (kernels.hip Geo::FPW)
+void chain_schedule(const int32_t* b, int nf, int L, int F, ChainSched& cs) {
   std::vector<int> lo(nf), len(nf);
   std::vector<int> order;
   for (int j = 0; j < nf; ++j) {
-    lo[j] = std::min<int>(b[j], L);
-    len[j] = std::max(0, std::min<int>(b[j + 2], L) - lo[j]);
+    const int first = std::min<int>(b[j], L), end = std::min<int>(b[j + 2], L);
+    lo[j] = first / 4 * 4;
+    len[j] = std::max(0, end - lo[j]);
     order.push_back(j);  // (an empty band too: its chain of zero weights stores the reference's 0)
   }
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return len[x] > len[y]; });
@@ -324,7 +326,7 @@ void chain_schedule(const int32_t* b, int nf, int L, ChainSched& cs) {
     cs.len[ph] = lp;
     for (int i = first; i < last; ++i) {
       const int j = order[i];
-      const int s0 = std::min(lo[j], L - lp), off = (int)cs.w.size();
+      const int s0 = std::min(lo[j], L - lp), off = (int)cs.w.size();  // (L and lp multiples of 8)
       for (int s = 0; s < lp; ++s) {
         const int k = s0 + s;
         double w = 0.0;
@@ -381,7 +383,11 @@ struct mgx_plan {
   int cus = 0;  // compute units of the plan's device
   int mel_zero = 1;  // some mel segment is empty (kernels.hip mel_energies)
   int chain_nph = 0;  // MGX_FLAG_MFCC_REFERENCE at N <= 1024: phases of the mel chains (chain_schedule)
+  int chain_pair = 0;  // ... over two consecutive batches of a wave (8 frames)
   int chain_len[mgx::kMaxChainPhases] = {0, 0, 0, 0};
+  // the mel chains' power-row rings (kernels.hip KGeo::GROWS), one per stream a launch used: the
+  // launches of one stream run in order, those of two streams may overlap
+  std::vector<std::pair<void*, float*>> chain_rings;
   // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
   float* s_frames[2] = {nullptr, nullptr};
   unsigned char* s_out[2] = {nullptr, nullptr};
@@ -502,7 +508,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   const bool chain = (d->flags & MGX_FLAG_MFCC_REFERENCE) && d->mode == MGX_MODE_PER_BUFFER_FFT &&
                      d->precision == MGX_PRECISION_FAITHFUL && n <= mgx::kChainMaxN;
   ChainSched cs;
-  if (chain) chain_schedule(bins.data(), nf, L, cs);
+  const bool pair = chain && nf <= mgx::kChainPairMaxMel;
+  if (chain) chain_schedule(bins.data(), nf, L, pair ? 8 : 4, cs);
 
   auto* p = new mgx_plan();
   p->d = *d;
@@ -522,6 +529,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   // persistent grid: exactly the workgroups that are resident at once
   p->grid_cap = prop.multiProcessorCount * std::max(1, mgx::extract_blocks_per_cu(n, (int)d->precision, (int)d->mode, (int)d->num_mfcc_coeffs, (int)d->num_mel_bands, chain));
   p->chain_nph = cs.nph;
+  p->chain_pair = pair;
   for (int i = 0; i < mgx::kMaxChainPhases; ++i) p->chain_len[i] = cs.len[i];
   p->cus = prop.multiProcessorCount;
   // (tuning knob: MGX_GRID_CAP overrides the persistent grid's size; MGX_GRID_CAP=print reports it)
@@ -574,6 +582,8 @@ int mgx_plan_destroy(mgx_plan* p) {
   if (!p) return MGX_OK;
   (void)hipSetDevice(p->d.device);
   if (p->dev) (void)hipFree(p->dev);
+  if (!p->chain_rings.empty()) (void)hipDeviceSynchronize();
+  for (auto& r : p->chain_rings) (void)hipFree(r.second);
   if (p->s_copy) (void)hipStreamSynchronize(p->s_copy);
   if (p->s_comp) (void)hipStreamSynchronize(p->s_comp);
   for (int i = 0; i < 2; ++i) {
@@ -619,6 +629,7 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.mfcc_reference = (p->d.flags & MGX_FLAG_MFCC_REFERENCE) ? 1 : 0;
   a.mel_zero = p->mel_zero;
   a.chain_nph = p->chain_nph;
+  a.chain_pair = p->chain_pair;
   for (int i = 0; i < mgx::kMaxChainPhases; ++i) a.chain_len[i] = p->chain_len[i];
   bool spec = o->loudness_specific || o->mfcc || o->amplitude_spectrum || o->power_spectrum || o->complex_real;
   for (int i = MGX_SPECTRAL_CENTROID; i < MGX_NUM_SCALARS; ++i) spec = spec || o->scalars[i];
@@ -639,6 +650,17 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.wg_ranks = grid == p->grid_cap && p->cus > 0 ? p->grid_cap / p->cus : 1;
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if (a.chain_nph > 0 && a.need_spectrum && a.need_mfcc) {
+    for (auto& r : p->chain_rings)
+      if (r.first == stream) a.chain_rows = r.second;
+    if (!a.chain_rows) {
+      // 2 FPW x N/2 floats for each wave of the largest grid (4 waves per workgroup)
+      const size_t bytes = (size_t)p->grid_cap * 4 * 2 * (size_t)(fb / 4) * (size_t)p->L * sizeof(float);
+      e = hipMalloc(reinterpret_cast<void**>(&a.chain_rows), bytes);
+      if (e != hipSuccess) return hip_fail(e, "hipMalloc(mel chain rows)");
+      p->chain_rings.emplace_back(stream, a.chain_rows);
+    }
+  }
   e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "extract kernel launch");
   return MGX_OK;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Mel chains over the device-memory ring (paired batches) against the round-3 LDS-row chains
+# (ab/libchain_lds.so) and the default plan: the chain GPU tests first, then A/B timing with
+# outputs compared bit for bit.
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+O=$R/gpurun_out/chain_g
+mkdir -p $O && cd $R
+timeout -k 10 400 python -u -m pytest tests/test_gpu_mfcc_chain.py tests/test_gpu_parity.py -k "chain or mfcc_reference" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+for n in 1024 512 256; do
+  timeout -k 10 300 python tools/ab_libs.py --n $n --rounds 5 --compare REF_L=ab/libchain_lds.so:2 REF_G=base:2 DEF=base > $O/ab_$n.log 2>&1 || { tail -20 $O/ab_$n.log; exit 1; }
+  grep -v amdgpu.ids $O/ab_$n.log | sed "s/^/N=$n /"
+done
