@@ -66,6 +66,9 @@ PATCHES = {
                 "      if (opaque(0)) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);"),
                ("      else run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);",
                 "      else if (opaque(0)) run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);")],
+    # two workgroup barriers per frame at the mel step (the cost of synchronising the workgroup's
+    # four waves once per frame; timing only, the batch size must give every wave the same count)
+    "bar2": [("  MGX_MARK(bands_done);\n", "  MGX_MARK(bands_done);\n  if (!CHAIN) { lds_barrier(); lds_barrier(); }\n")],
     "no_mel": [("  } else if (!CHAIN && ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && !CHAIN && ap->need_mfcc) {\n    mel_energies")],
 }
 
