@@ -1053,7 +1053,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       for (int c = 0; c < CH; ++c) xn[c] = ld_frame(next + (c * 64 + (unsigned)lane));
     }
   };
-  if (!ap->need_spectrum) prefetch_next();  // time-only features: no table loads follow
   // The window: held in registers for the launch at N = 1024 (Geo::WIN_REG); otherwise its
   // table loads are issued before the energy / zcr reductions, so their latency hides behind
   // them rather than at the window step after the reductions' branches (1 % faster at
@@ -1132,7 +1131,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     recs[fb].energy = e;
     recs[fb].zcr = z;
   }
-  if (!ap->need_spectrum) {  // (the prefetch was issued at the top: nothing to wait on)
+  if (!ap->need_spectrum) {  // time-only features: the next frame now (its registers are free)
+    prefetch_next();
     prio_lo<16>();
     return;
   }
