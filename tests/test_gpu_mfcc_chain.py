@@ -106,3 +106,24 @@ def test_chain_large_batch_sample(capi, oracle_mod):
     frac, _ = _mfcc_reference_checks(out["mfcc"].cpu().numpy()[idx], out["amplitudeSpectrum"].cpu().numpy()[idx],
                                      ref["mfcc"], ref["amp"])
     assert frac >= 0.95, frac
+
+
+@pytest.mark.parametrize("reference", [False, True])
+def test_one_launch_equals_small_launches(capi, reference):
+    """Frames are independent, so one launch over 40,963 frames -- waves of 3 batches each (with
+    the reference order: a pair of batches whose chains run together, then a last batch finished
+    alone after the loop), the last group of batches partial (its missing batches run on the
+    clamped last frame and store nothing) -- equals the same frames extracted in launches of 997
+    frames, every output bit for bit."""
+    n, F, step = 1024, 40963, 997
+    rng = np.random.default_rng(7)
+    x = rng.uniform(-1, 1, (F, n)).astype(np.float32)
+    t = np.arange(n) / 44100.0
+    for i in range(0, F, 5):
+        x[i] = (rng.uniform(0.01, 0.9) * np.sin(2 * np.pi * rng.uniform(30, 18000) * t)).astype(np.float32)
+    plan = capi.Plan(buffer_size=n, scalar_f64=True, mfcc_reference=reference)
+    full = plan.extract(x, FEATS)
+    parts = [plan.extract(x[i:i + step], FEATS) for i in range(0, F, step)]
+    for k, v in full.items():
+        joined = np.concatenate([p[k] for p in parts])
+        assert np.array_equal(v.view(np.uint8), joined.view(np.uint8)), k
