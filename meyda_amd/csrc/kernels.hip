@@ -1972,6 +1972,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     prio_lo<4>();
     MGX_MARK(phase2_end);
     wave_sync();  // records and slot buffer are reused by the next batch
+#if MGX_GROUP_SYNC
+    // every wave of the workgroup has a batch in this group (the same full groups for all four,
+    // so the barrier counts match): the group's output lines are written together
+    if ((b - wave) + 3 < nb) __builtin_amdgcn_s_barrier();
+#endif
   }
   if constexpr (CHAIN) {
     // paired batches: a wave whose last batch opened a pair finishes that batch's mfcc alone
