@@ -129,6 +129,9 @@ struct Geo {
   // frame loop spills)
   static constexpr bool BLIM_REG = N <= 512;
   static constexpr bool PREFETCH = PF != 0;
+  // GROUP_SYNC: a workgroup barrier after every GROUP_SYNC-th full group of 16 frames, so the
+  // group's output lines are written together (extract_kernel; 0 = none)
+  static constexpr int GROUP_SYNC = N == 2048 ? 0 : 2;
   static constexpr bool LPREMAT = N == 2048;  // measured: N = 2048 1 % faster, N = 256 7 % slower
   static constexpr int MIX = 1;  // bfly_mixed_tame (form 0 was faster at N = 1024 at 128 live VGPRs)
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
@@ -982,51 +985,64 @@ __device__ __forceinline__ void mel_reference_order(KArgs* ap, const float (&av)
 // ascending order, the weight (an IEEE double quotient, plan table) times the float32 power rounded
 // to double, added to the Float32Array element in double and stored back to float32 -- exactly the
 // reference's operations, so the sums are the reference's bits. The host schedule (plan.cpp
-// chain_schedule) puts 64 chains side by side per phase, a band's F frames in one phase, every lane
-// of a phase running its length from a 4-aligned first bin (16-byte row loads).
+// chain_schedule) packs the chains into 64 / F tracks of F lanes (one lane per frame), each track
+// running its bands' chains back to back in groups of 8 steps; per group and lane a control word
+// gives the row offset, whether a chain starts (its first step adds to 0) and where the chain that
+// ends there is stored (a FrameRec::lm entry, or the lane's scratch word in the slot buffer, which
+// is free in phase 2).
 //   F = 8 (KernelArgs::chain_pair, nfilt <= 31): the chains of two consecutive batches of the wave
 //     run together, in the second batch's phase 2 (ring slots 0..3 the first batch, 4..7 the
-//     second): the longest band (120 bins at N = 1024, 26 bands) is then shared by 8 frames instead
-//     of 4, and the lanes are busy for most of its length. The first batch's energies go to the
-//     upper half of its records' lm (lm[32 + band]); lm[31] / lm[63] hold the frame's non-finite
-//     flag (its energies then come from nonfinite_frame_sums). have_cur = false (the wave's last
-//     batch was the first of a pair) stores only the first batch's.
+//     second): the first batch's energies go to the upper half of its records' lm (lm[32 + band]);
+//     lm[31] / lm[63] hold the frame's non-finite flag. have_cur = false (the wave's last batch was
+//     the first of a pair): the second batch's chains run on stale rows into lm[band] of records
+//     nobody reads.
 //   F = 4 (more bands): the batch's chains in its own phase 2, slots 0..3, the non-finite flag a bit
 //     of the record's zcr count.
-// Per step: the conversion, product, sum and the two roundings on the VALU; per 8 steps two 16-byte
-// row loads and the 8 weights.
+// A non-finite frame's energies (nonfinite_frame_sums) wait at the start of its ring slot and are
+// put back after the chains. Per step: the conversion, product, sum and the two roundings on the
+// VALU; per group two 16-byte row loads, the 8 weights (shared by the track's F lanes), the next
+// control word and one LDS store.
 template <int N>
-__device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec* recs, bool pair, bool have_cur) {
+__device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec* recs, float2* buf, bool pair, bool have_cur) {
   constexpr int L = N / 2;
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) f32x4* GF4;
-  const auto cl = gbl(reinterpret_cast<const uint32_t*>(q->t.chain_lane));
-  const auto cw = gbl(q->t.chain_w);
-  for (int ph = 0; ph < q->chain_nph; ++ph) {
-    const uint32_t rx = cl[2 * (ph * 64 + lane)], ry = cl[2 * (ph * 64 + lane) + 1];
-    const int s0 = (int)(rx & 0xFFFu), fr = (int)((rx >> 12) & 7u), band = (int)((rx >> 16) & 0x7Fu);
-    const GF4 pr = (GF4)(ring + fr * L + s0);  // s0 is a multiple of 4 (chain_schedule)
-    const auto wp = cw + ry;
-    const int len = q->chain_len[ph];
-    double acc = 0.0;  // the Float32Array element, held exactly in double
-    for (int s = 0; s < len; s += 8) {
-      const f32x4 p0 = pr[s / 4], p1 = pr[s / 4 + 1];
-      const float p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-      double w[8];
+  static_assert(sizeof(FrameRec) == kRecBytes && offsetof(FrameRec, lm) == kRecLmOff, "chain_schedule's record offsets");
+  const auto ctl = gbl(q->t.chain_ctl);
+  const int ng = q->chain_groups, F = pair ? 8 : 4;
+  const auto wp = gbl(q->t.chain_w) + (lane / F) * (ng * 8);
+  unsigned char* const rb = reinterpret_cast<unsigned char*>(recs);
+  float* const scratch = reinterpret_cast<float*>(buf) + lane;
+  auto store = [&](uint32_t c, double acc) {
+    float* dst = (c & (1u << 26)) ? reinterpret_cast<float*>(rb + ((c >> 13) & 0xFFFu)) : scratch;
+    *dst = (float)acc;
+  };
+  double acc = 0.0;  // the Float32Array element, held exactly in double
+  uint32_t c = ctl[lane];
+  for (int g = 0; g < ng; ++g) {
+    const uint32_t cn = ctl[(g + 1) * 64 + lane];  // (the last chain's store after the loop)
+    const GF4 pr = (GF4)(ring + (c & 0x1FFFu));      // a multiple of 4 floats (chain_schedule)
+    const f32x4 p0 = pr[0], p1 = pr[1];
+    const float p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+    double w[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) w[u] = wp[s + u];
+    for (int u = 0; u < 8; ++u) w[u] = wp[g * 8 + u];
+    store(c, acc);  // the chain that ends here (or the scratch word)
+    // a chain starting here adds its first product to 0 (a select: acc may be an overflowed +inf)
+    const double a0 = (c & (1u << 25)) ? 0.0 : acc;
+    acc = (double)(float)(a0 + w[0] * (double)p[0]);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc = (double)(float)(acc + w[u] * (double)p[u]);  // two roundings, the float32 store
-    }
-    if ((int)rx < 0) {
-      if (!pair) {
-        if (!(recs[fr].zcr & kChainSkip)) recs[fr].lm[band] = (float)acc;
-      } else {
-        FrameRec& r = recs[fr & 3];
-        const int lmo = fr < 4 ? 32 : 0;  // the pair's first batch: the upper half
-        if ((fr < 4 || have_cur) && r.lm[lmo + 31] == 0.0f) r.lm[lmo + band] = (float)acc;
-      }
-    }
+    for (int u = 1; u < 8; ++u) acc = (double)(float)(acc + w[u] * (double)p[u]);  // two roundings, the float32 store
+    c = cn;
+  }
+  store(c, acc);
+  // the non-finite frames' own sums back from their ring slots (wave-uniform, rare)
+  wave_sync();
+  for (int fr = 0; fr < F; ++fr) {
+    FrameRec& r = recs[fr & 3];
+    const int lmo = pair && fr < 4 ? 32 : 0;
+    const bool nf = pair ? r.lm[lmo + 31] != 0.0f : (r.zcr & kChainSkip) != 0;
+    if (nf && (!pair || fr < 4 || have_cur) && lane < q->nfilt) r.lm[lmo + lane] = ring[fr * L + lane];
   }
 }
 
@@ -1468,14 +1484,21 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
   if constexpr (CHAIN) {
     // the frame's power row (powerSpectrum.js) for the mel chains in phase 2 (mel_chains): ring slot
-    // fb, or with paired batches 4 (it & 1) + fb; a non-finite frame keeps the mel sums
-    // nonfinite_frame_sums formed (its flag: lm[31] of its half, or a bit of its zcr count)
+    // fb, or with paired batches 4 (it & 1) + fb. A non-finite frame keeps the mel sums
+    // nonfinite_frame_sums formed (its flag: lm[31] of its half, or a bit of its zcr count): they go
+    // to the start of its ring slot instead, and mel_chains puts them back after its chains
+    // (whose stores do not look at the flag).
     if (ap->need_mfcc) {
       const bool pair = ap->chain_pair;
       // (the wave's ring in device memory: R consecutive floats per lane)
       auto row = gbl(rows) + ((pair ? 4 * (it & 1) : 0) + fb) * L;
+      if (nonfinite) {
+        wave_sync();
+        if (lane < ap->nfilt) row[lane] = rec.lm[(pair && !(it & 1) ? 32 : 0) + lane];
+      } else {
 #pragma unroll
-      for (int jj = 0; jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];
+        for (int jj = 0; jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];
+      }
       if (pair) {
         if (lane == 0) rec.lm[(it & 1 ? 0 : 32) + 31] = nonfinite ? 1.0f : 0.0f;
       } else if (nonfinite && lane == 0) {
@@ -1896,7 +1919,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         // wave's alone and the CU's L1 is coherent for its own waves (workgroup scope)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        mel_chains<N>(q, opaque(lane), gbl(rows), recs, q->chain_pair, true);
+        mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);
         wave_sync();  // the band energies are in the records: the log step reads them
       }
     }
@@ -1972,11 +1995,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     prio_lo<4>();
     MGX_MARK(phase2_end);
     wave_sync();  // records and slot buffer are reused by the next batch
-#if MGX_GROUP_SYNC
-    // every wave of the workgroup has a batch in this group (the same full groups for all four,
-    // so the barrier counts match): the group's output lines are written together
-    if ((b - wave) + 3 < nb) __builtin_amdgcn_s_barrier();
-#endif
+    // The workgroup's four waves meet after every second group of 16 frames (G::GROUP_SYNC).
+    // Left alone they drift apart by more than the L2's turnover time, so each wave's 16-byte piece
+    // of a 64-byte scalar line was written back on its own: WRITE_SIZE 1.13x the outputs (time-only
+    // set 1.40x). With the barrier: 1.016x (1.10x), all-feature launch +0.0 %, time-only -3.8 %,
+    // outputs identical (profiles/r03_group_sync.txt). Every wave has a batch in a full group, so
+    // all four reach the same barriers. N = 2048 (3 waves per SIMD) lost 2.3 % and keeps none.
+    if constexpr (G::GROUP_SYNC > 0) {
+      const uint64_t g = (b - wave) / 4;
+      if (g * 4 + 3 < nb && g % G::GROUP_SYNC == G::GROUP_SYNC - 1) __builtin_amdgcn_s_barrier();
+    }
   }
   if constexpr (CHAIN) {
     // paired batches: a wave whose last batch opened a pair finishes that batch's mfcc alone
@@ -1986,7 +2014,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       const int l2 = opaque(lane);
-      mel_chains<N>(q, l2, gbl(rows), recs, true, false);
+      mel_chains<N>(q, l2, gbl(rows), recs, buf, true, false);
       wave_sync();
       mfcc_log<CHAIN, SUB>(q, l2, recs, 32);
       wave_sync();
@@ -2110,7 +2138,7 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
   const bool every = a.need_mom == 2 && a.need_prefix && a.need_energy && a.need_zcr;
   if constexpr (kChainN<N>) {
     // MGX_FLAG_MFCC_REFERENCE: the mel sums as chains in the reference's order (mel_chains)
-    if (a.chain_nph > 0 && a.need_spectrum && a.need_mfcc) {
+    if (a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) {
       if (every) return launch_n<N, true, false, false, false, false, true>(a, grid, stream);
       return launch_n<N, true, false, true, false, false, true>(a, grid, stream);
     }

@@ -13,8 +13,9 @@ constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
 constexpr int kMelHead = kMaxMel + 2;  // mel scratch: segment sums [0, nfilt + 2), head partials from here
 // Mel band chains in the reference's own order (MGX_FLAG_MFCC_REFERENCE, N <= 1024): F frames x
-// nfilt chains, 64 per phase (F = 8 for nfilt <= 31, else F = 4), so at most 4 phases.
-constexpr int kMaxChainPhases = 4;
+// nfilt chains on 64 / F packed tracks (F = 8 for nfilt <= 31, else F = 4; plan.cpp chain_schedule).
+constexpr int kRecBytes = 520;  // sizeof(FrameRec) (kernels.hip)
+constexpr int kRecLmOff = 248;  // offsetof(FrameRec, lm)
 constexpr int kChainPairMaxMel = 31;  // paired batches keep two halves of FrameRec::lm (flag at 31)
 constexpr int kChainMaxN = 1024;
 constexpr int kChainSkip = 1 << 30;  // FrameRec.zcr flag bit: a non-finite frame keeps its phase-1 mel sums
@@ -33,8 +34,8 @@ struct DevTables {
   const int* mel_bins;       // nfilt + 2 filter edges (mfcc.js:15-38), for the non-finite-frame path
   const float* dct;          // ncoef * nfilt, dct[c + j*ncoef] (mfcc.js:67-83)
   // MGX_FLAG_MFCC_REFERENCE at N <= 1024 (plan.cpp chain_schedule, kernels.hip mel_chains):
-  const uint2* chain_lane;   // per phase and lane: (first bin | frame << 12 | band << 16 | valid << 31, weight offset)
-  const double* chain_w;     // per band, the weights of its chain steps (zero-padded to its phase's length)
+  const uint32_t* chain_ctl; // per 8-step group and lane: row offset, chain start, the finished chain's store
+  const double* chain_w;     // per track, the weights of its chains' steps back to back
 };
 
 struct KernelArgs {
@@ -62,8 +63,7 @@ struct KernelArgs {
   int mfcc_reference;    // MGX_FLAG_MFCC_REFERENCE: mel sums, log and DCT in the reference's order (SUB kernel)
   int mel_zero;          // some mel segment [b_m, b_{m+1}) is empty: the scan's slots are zeroed first
   int wg_ranks;          // workgroups per CU when the grid is the resident one (else 1): their work shares
-  int chain_nph;         // phases of the mel chain schedule (0: the segmented scan)
-  int chain_len[kMaxChainPhases];  // steps of each phase (multiples of 8)
+  int chain_groups;      // 8-step groups of the mel chain tracks (0: the segmented scan)
   int chain_pair;        // the chains of two consecutive batches of a wave run together (8 frames, nfilt <= 31)
   float* chain_rows;     // the chains' power rows: 2 FPW x N/2 floats per wave of the grid (kernels.hip mel_chains)
 };

@@ -291,54 +291,82 @@ void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& 
 // mfcc.js:43-50 -- (k - b_j) / (b_{j+1} - b_j) rising, (b_{j+2} - k) / (b_{j+2} - b_{j+1}) falling,
 // IEEE double quotients as JavaScript forms them -- and the float32 accumulator (every other bin
 // adds an exact +0 in the reference for a finite spectrum). F frames x nf such chains run together
-// (F = 8: two consecutive batches of a wave, when nf <= kChainPairMaxMel; else the batch's 4);
-// sorted by length they fill phases of 64 lanes (64 / F bands x the F frames: a band's chains
-// share a phase, its length the longest chain of the phase rounded up to 8 steps). A lane reads Lp
-// consecutive bins from its first bin, which is a multiple of 4 (16-byte row loads): a chain starts
-// at its first bin rounded down to 4, or earlier if it would run past N/2, with leading zero
-// weights (a zero weight times a finite power adds +0).
-// Lanes without a chain read a table of zeros and store nothing; a band without bins (low bands
-// of many-band plans) has a chain of zero weights, so its energy is the reference's 0.
-//   lane record: (first bin | frame << 12 | band << 16 | 1 << 31, offset of the band's weights)
+// (F = 8: two consecutive batches of a wave, when nf <= kChainPairMaxMel; else the batch's 4).
+// A chain runs in whole groups of 8 steps from its first bin rounded down to 4 (16-byte row loads),
+// or earlier if it would run past N/2, with leading zero weights (a zero weight times a finite
+// power adds +0); a band without bins (low bands of many-band plans) has one group of zero
+// weights, so its energy is the reference's 0.
+// Packed tracks: the 64 lanes are 64 / F tracks x the F frames (lane = track * F + frame). The
+// bands are dealt to the tracks longest first, each to the least loaded track, and a track runs its
+// bands' chains back to back, so the lanes stay busy for ngroups = the largest track load (N = 1024,
+// 26 bands: 18 groups instead of the 24 of phases whose length is the phase's longest chain).
+//   ctl[g * 64 + lane], g < ngroups (the lane's row and what happens at the group's start):
+//     bits 0-12 the row offset in floats (frame * L + bin), bit 25 a chain starts here (its first
+//     step adds to 0), bit 26 the finished chain before it is
+//     stored at bits 13-24 (a byte offset into the wave's frame records: FrameRec::lm of its frame
+//     and band); without bit 26 the store goes to the lane's scratch word.
+//   ctl[ngroups * 64 + lane]: the store of the lane's last chain (bit 26 and bits 13-24 only).
+//   w[track * ngroups * 8 + s]: the weight of the track's step s (0 past its last chain).
 struct ChainSched {
-  int nph = 0;
-  int len[mgx::kMaxChainPhases] = {0, 0, 0, 0};
-  std::vector<uint32_t> lane;  // 2 dwords per (phase, lane)
+  int ngroups = 0;
+  std::vector<uint32_t> ctl;
   std::vector<double> w;
 };
 void chain_schedule(const int32_t* b, int nf, int L, int F, ChainSched& cs) {
-  std::vector<int> lo(nf), len(nf);
-  std::vector<int> order;
+  const int ntr = 64 / F;
+  std::vector<int> lo(nf), len(nf), order;
   for (int j = 0; j < nf; ++j) {
     const int first = std::min<int>(b[j], L), end = std::min<int>(b[j + 2], L);
     lo[j] = first / 4 * 4;
-    len[j] = std::max(0, end - lo[j]);
-    order.push_back(j);  // (an empty band too: its chain of zero weights stores the reference's 0)
+    len[j] = std::max(8, (std::max(0, end - lo[j]) + 7) / 8 * 8);
+    if (lo[j] + len[j] > L) lo[j] = L - len[j];  // (L and len multiples of 8)
+    order.push_back(j);
   }
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return len[x] > len[y]; });
-  const int per = 64 / F;  // bands per phase
-  cs.nph = ((int)order.size() + per - 1) / per;
-  cs.lane.assign((size_t)mgx::kMaxChainPhases * 128, 0u);
-  cs.w.assign((size_t)L, 0.0);  // [0, L): the zero table of idle lanes
-  for (int ph = 0; ph < cs.nph; ++ph) {
-    const int first = ph * per, last = std::min((int)order.size(), first + per);
-    const int lp = std::min(L, (len[order[first]] + 7) / 8 * 8);
-    cs.len[ph] = lp;
-    for (int i = first; i < last; ++i) {
-      const int j = order[i];
-      const int s0 = std::min(lo[j], L - lp), off = (int)cs.w.size();  // (L and lp multiples of 8)
-      for (int s = 0; s < lp; ++s) {
-        const int k = s0 + s;
-        double w = 0.0;
-        if (k >= b[j] && k < b[j + 1] && k < L) w = (double)(k - b[j]) / (double)(b[j + 1] - b[j]);
-        else if (k >= b[j + 1] && k < b[j + 2] && k < L) w = (double)(b[j + 2] - k) / (double)(b[j + 2] - b[j + 1]);
-        cs.w.push_back(w);
+  std::vector<std::vector<int>> track(ntr);
+  std::vector<int> load(ntr, 0);
+  for (int j : order) {
+    int t = 0;
+    for (int u = 1; u < ntr; ++u)
+      if (load[u] < load[t]) t = u;
+    track[t].push_back(j);
+    load[t] += len[j];
+  }
+  const int ng = *std::max_element(load.begin(), load.end()) / 8;
+  cs.ngroups = ng;
+  cs.ctl.assign((size_t)(ng + 1) * 64, 0u);
+  cs.w.assign((size_t)ntr * ng * 8, 0.0);
+  auto target = [&](int j, int f) {  // byte offset of FrameRec::lm[band (+32: a pair's first batch)]
+    const int lmo = (F == 8 && f < 4) ? 32 : 0;
+    return (uint32_t)((f & 3) * mgx::kRecBytes + mgx::kRecLmOff + 4 * (j + lmo)) << 13 | 1u << 26;
+  };
+  for (int t = 0; t < ntr; ++t) {
+    double* w = cs.w.data() + (size_t)t * ng * 8;
+    int g0 = 0;
+    for (size_t c = 0; c < track[t].size(); ++c) {
+      const int j = track[t][c];
+      for (int s = 0; s < len[j]; ++s) {
+        const int k = lo[j] + s;
+        double v = 0.0;
+        if (k >= b[j] && k < b[j + 1] && k < L) v = (double)(k - b[j]) / (double)(b[j + 1] - b[j]);
+        else if (k >= b[j + 1] && k < b[j + 2] && k < L) v = (double)(b[j + 2] - k) / (double)(b[j + 2] - b[j + 1]);
+        w[g0 * 8 + s] = v;
       }
       for (int f = 0; f < F; ++f) {
-        const int ln = (i - first) * F + f;
-        cs.lane[(size_t)ph * 128 + 2 * ln] = (uint32_t)s0 | (uint32_t)f << 12 | (uint32_t)j << 16 | 1u << 31;
-        cs.lane[(size_t)ph * 128 + 2 * ln + 1] = (uint32_t)off;
+        const int lane = t * F + f;
+        for (int g = g0; g < g0 + len[j] / 8; ++g) {
+          uint32_t c32 = (uint32_t)(f * L + lo[j] + 8 * (g - g0));
+          if (g == g0) c32 |= 1u << 25 | (c > 0 ? target(track[t][c - 1], f) : 0u);
+          cs.ctl[(size_t)g * 64 + lane] = c32;
+        }
       }
+      g0 += len[j] / 8;
+    }
+    for (int f = 0; f < F; ++f) {
+      const int lane = t * F + f;
+      // past the track's last chain: bin 0 of the frame with zero weights (adds +0); no reset
+      for (int g = g0; g < ng; ++g) cs.ctl[(size_t)g * 64 + lane] = (uint32_t)(f * L);
+      cs.ctl[(size_t)ng * 64 + lane] = track[t].empty() ? 0u : target(track[t].back(), f);
     }
   }
 }
@@ -382,9 +410,8 @@ struct mgx_plan {
   int grid_cap = 1;
   int cus = 0;  // compute units of the plan's device
   int mel_zero = 1;  // some mel segment is empty (kernels.hip mel_energies)
-  int chain_nph = 0;  // MGX_FLAG_MFCC_REFERENCE at N <= 1024: phases of the mel chains (chain_schedule)
+  int chain_groups = 0;  // MGX_FLAG_MFCC_REFERENCE at N <= 1024: 8-step groups of the mel chains (chain_schedule)
   int chain_pair = 0;  // ... over two consecutive batches of a wave (8 frames)
-  int chain_len[mgx::kMaxChainPhases] = {0, 0, 0, 0};
   // the mel chains' power-row rings (kernels.hip KGeo::GROWS), one per stream a launch used: the
   // launches of one stream run in order, those of two streams may overlap
   std::vector<std::pair<void*, float*>> chain_rings;
@@ -528,9 +555,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   for (int i = 15; i < mgx::kBark; ++i) p->sharp_tail += 0.066 * exp(0.171 * (i + 1));  // perceptualSharpness.js:10
   // persistent grid: exactly the workgroups that are resident at once
   p->grid_cap = prop.multiProcessorCount * std::max(1, mgx::extract_blocks_per_cu(n, (int)d->precision, (int)d->mode, (int)d->num_mfcc_coeffs, (int)d->num_mel_bands, chain));
-  p->chain_nph = cs.nph;
+  p->chain_groups = cs.ngroups;
   p->chain_pair = pair;
-  for (int i = 0; i < mgx::kMaxChainPhases; ++i) p->chain_len[i] = cs.len[i];
   p->cus = prop.multiProcessorCount;
   // (tuning knob: MGX_GRID_CAP overrides the persistent grid's size; MGX_GRID_CAP=print reports it)
   if (const char* gc = getenv("MGX_GRID_CAP")) {
@@ -543,7 +569,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
                o_twf = carve<float>(off, twf.size()), o_twm = carve<double>(off, twm.size()),
                o_kl = carve<int>(off, L),
                o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<uint32_t>(off, mrec.size()), o_dct = carve<float>(off, dct.size()),
-               o_mb = carve<int32_t>(off, bins.size()), o_cl = carve<uint32_t>(off, cs.lane.size()),
+               o_mb = carve<int32_t>(off, bins.size()), o_cl = carve<uint32_t>(off, cs.ctl.size()),
                o_cw = carve<double>(off, cs.w.size());
   std::vector<unsigned char> host(off, 0);
   auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) memcpy(host.data() + at, src, bytes); };
@@ -556,7 +582,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   put(o_mw, mrec.data(), mrec.size() * sizeof(uint32_t));
   put(o_mb, bins.data(), bins.size() * sizeof(int32_t));
   put(o_dct, dct.data(), dct.size() * sizeof(float));
-  put(o_cl, cs.lane.data(), cs.lane.size() * sizeof(uint32_t));
+  put(o_cl, cs.ctl.data(), cs.ctl.size() * sizeof(uint32_t));
   put(o_cw, cs.w.data(), cs.w.size() * sizeof(double));
   e = hipMalloc(reinterpret_cast<void**>(&p->dev), off);
   if (e != hipSuccess) { delete p; return hip_fail(e, "hipMalloc(plan tables)"); }
@@ -572,7 +598,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->t.mel_rec = reinterpret_cast<const uint32_t*>(b + o_mw);
   p->t.mel_bins = reinterpret_cast<const int*>(b + o_mb);
   p->t.dct = reinterpret_cast<const float*>(b + o_dct);
-  p->t.chain_lane = reinterpret_cast<const uint2*>(b + o_cl);
+  p->t.chain_ctl = reinterpret_cast<const uint32_t*>(b + o_cl);
   p->t.chain_w = reinterpret_cast<const double*>(b + o_cw);
   *out = p;
   return MGX_OK;
@@ -628,9 +654,8 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.dct_sequential = (p->d.flags & MGX_FLAG_DCT_SEQUENTIAL) ? 1 : 0;
   a.mfcc_reference = (p->d.flags & MGX_FLAG_MFCC_REFERENCE) ? 1 : 0;
   a.mel_zero = p->mel_zero;
-  a.chain_nph = p->chain_nph;
+  a.chain_groups = p->chain_groups;
   a.chain_pair = p->chain_pair;
-  for (int i = 0; i < mgx::kMaxChainPhases; ++i) a.chain_len[i] = p->chain_len[i];
   bool spec = o->loudness_specific || o->mfcc || o->amplitude_spectrum || o->power_spectrum || o->complex_real;
   for (int i = MGX_SPECTRAL_CENTROID; i < MGX_NUM_SCALARS; ++i) spec = spec || o->scalars[i];
   a.need_spectrum = spec;
@@ -650,7 +675,7 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.wg_ranks = grid == p->grid_cap && p->cus > 0 ? p->grid_cap / p->cus : 1;
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  if (a.chain_nph > 0 && a.need_spectrum && a.need_mfcc) {
+  if (a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) {
     for (auto& r : p->chain_rings)
       if (r.first == stream) a.chain_rows = r.second;
     if (!a.chain_rows) {

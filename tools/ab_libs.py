@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--frames", type=int, default=262144)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--features", default="all")
+    ap.add_argument("--mel", type=int, default=26, help="mel bands of every plan")
     ap.add_argument("--precision", default="faithful", choices=["faithful", "fast"])
     ap.add_argument("--compare", action="store_true", help="also check every variant's outputs against the first's, bit for bit")
     ap.add_argument("variants", nargs="+")
@@ -39,7 +40,7 @@ def main():
     x = torch.empty(F, n, dtype=torch.float32, device="cuda")
     capi.synth_frames_device(x, 0x6D657964)
     feats = capi.ALL_FEATURES if a.features == "all" else a.features.split(",")
-    plan0 = capi.Plan(buffer_size=n, precision=a.precision)
+    plan0 = capi.Plan(buffer_size=n, precision=a.precision, num_mel_bands=a.mel)
     outs, o = plan0.alloc_outputs(F, feats)
     vs = []
     for spec in a.variants:
@@ -50,7 +51,7 @@ def main():
             flags = int(fl, 0)
         path = capi.LIB_PATH if path == "base" else path
         L = load(path)
-        d = capi.make_desc(buffer_size=n, precision=a.precision)
+        d = capi.make_desc(buffer_size=n, precision=a.precision, num_mel_bands=a.mel)
         d.flags = flags
         h = ctypes.c_void_p()
         rc = L.mgx_plan_create(ctypes.byref(d), ctypes.byref(h))

@@ -44,16 +44,16 @@ PATCHES = {
                    "  const bool need_prefix = opaque(0);")],
     # MGX_FLAG_MFCC_REFERENCE (CHAIN kernels): the chains skipped (the occupancy / LDS-layout /
     # power-row cost alone)
-    "chain_none": [("        mel_chains<N>(q, opaque(lane), gbl(rows), recs, q->chain_pair, true);",
-                    "        if (opaque(0)) mel_chains<N>(q, opaque(lane), gbl(rows), recs, q->chain_pair, true);")],
+    "chain_none": [("        mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);",
+                    "        if (opaque(0)) mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);")],
     # the CHAIN kernels' power-row stores to the device-memory ring skipped (the chains read stale rows)
     "chain_norows": [("      for (int jj = 0; jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];",
                       "      for (int jj = 0; opaque(0) && jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];")],
     # the fence before the chains (a vmcnt(0) wait: the next frame's prefetch, the row stores) dropped
     "chain_nofence": [("""        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        mel_chains<N>(q, opaque(lane), gbl(rows), recs, q->chain_pair, true);""",
-                       """        mel_chains<N>(q, opaque(lane), gbl(rows), recs, q->chain_pair, true);""")],
+        mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);""",
+                       """        mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);""")],
     # the FFT passes after pass 0 skipped (the exchanges too): what the f64 butterflies cost
     "no_passes": [("      if (tame) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);",
                    "      if (opaque(0)) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);"),
