@@ -284,9 +284,9 @@ struct KlTab {
 // HBM-bound time-only features 12 % faster on a 1 GiB batch (5.9 TB/s), but C2's 128 MiB batch
 // 12 % slower (with plain loads it stays resident in the 256 MiB MALL across launches), and
 // made no change where the kernel is VALU-bound.
-#ifndef MGX_CHAIN_NT
-#define MGX_CHAIN_NT 0
-#endif
+// NT: a non-temporal load (the CHAIN kernels' frames: the power-row ring keeps more of the L2;
+// -0.6..-1.2 % per reference-order launch, profiles/r03_mfcc_tracks.txt. The other kernels keep
+// plain loads: C2's batch stays in the MALL between launches, which nt loads lose)
 template <bool NT = false>
 __device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))) float* p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -1026,31 +1026,12 @@ __device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec
   };
   double acc = 0.0;  // the Float32Array element, held exactly in double
   uint32_t c = ctl[lane], cn = ctl[64 + lane];  // (the table has ng + 1 >= 2 rows)
-#if MGX_CHAIN_PF
-  // the next group's rows are loaded while this group's steps run (after this group's weights, so
-  // that waiting for the weights -- L2 hits -- does not wait for them: vmcnt counts in issue order)
-  f32x4 q0, q1;
-  {
-    const GF4 pr = (GF4)(ring + (c & 0x1FFFu));
-    q0 = pr[0];
-    q1 = pr[1];
-  }
-#endif
   for (int g = 0; g < ng; ++g) {
     double w[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) w[u] = wp[g * 8 + u];
-#if MGX_CHAIN_PF
-    const f32x4 p0 = q0, p1 = q1;
-    {
-      const GF4 pr = (GF4)(ring + ((g + 1 < ng ? cn : c) & 0x1FFFu));  // (the last group: its own rows again)
-      q0 = pr[0];
-      q1 = pr[1];
-    }
-#else
     const GF4 pr = (GF4)(ring + (c & 0x1FFFu));      // a multiple of 4 floats (chain_schedule)
     const f32x4 p0 = pr[0], p1 = pr[1];
-#endif
     const uint32_t cnn = ctl[(g + 2 < ng ? g + 2 : ng) * 64 + lane];
     const float p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
     store(c, acc);  // the chain that ends here (or the scratch word)
@@ -1093,7 +1074,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   auto prefetch_next = [&]() {
     if constexpr (G::PF == 2) {
 #pragma unroll
-      for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN && MGX_CHAIN_NT>(next + (c * 64 + (unsigned)lane));
+      for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN>(next + (c * 64 + (unsigned)lane));
     }
   };
   // The window: held in registers for the launch at N = 1024 (Geo::WIN_REG); otherwise its
@@ -1884,7 +1865,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   auto load = [&](float (&xv)[CH], uint64_t b, int j) {
     const GF xin = frame_ptr(b, j);
 #pragma unroll
-    for (int c = 0; c < CH; ++c) xv[c] = ld_frame<CHAIN && MGX_CHAIN_NT>(xin + (c * 64 + (unsigned)lane));
+    for (int c = 0; c < CH; ++c) xv[c] = ld_frame<CHAIN>(xin + (c * 64 + (unsigned)lane));
   };
 
   // the band lane's prefix-row offsets pd(lim[b]) | pd(lim[b + 1]) << 16 (G::BLIM_REG)
