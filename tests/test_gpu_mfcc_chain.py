@@ -127,3 +127,28 @@ def test_one_launch_equals_small_launches(capi, reference):
     for k, v in full.items():
         joined = np.concatenate([p[k] for p in parts])
         assert np.array_equal(v.view(np.uint8), joined.view(np.uint8)), k
+
+
+def test_chain_overflowing_band_then_next_chain(capi, oracle_mod):
+    """A finite frame whose widest mel band overflows float32 (three loud tones inside band 25 of
+    26 at N = 1024, bins 460 / 475 / 490, each bin's power finite): the reference's Float32Array
+    sum is +inf there, so every coefficient is +-inf (the DCT column's signs), not NaN. On the packed
+    tracks another band's chain follows band 25's on the same lanes; it must start from 0 (a
+    select), not from inf x 0 = NaN, or the coefficients would turn NaN."""
+    n = 1024
+    t = np.arange(n, dtype=np.float64)
+    rng = np.random.default_rng(11)
+    x = []
+    for a in (1.6e18, 1.9e18, 2.2e18):  # (jsfft scales by 2^-5 at N = 1024: peak |X| ~ 8 a)
+        y = sum(a * np.sin(2 * np.pi * k * t / n + rng.uniform(0, 6.28)) for k in (460, 475, 490))
+        x.append((y + rng.uniform(-1, 1, n)).astype(np.float32))
+    x = np.stack(x)
+    ref = oracle_mod.extract(x)
+    assert np.isfinite(ref["amp"]).all()
+    assert np.isinf(ref["mfcc"]).any() and not np.isnan(ref["mfcc"]).all(), ref["mfcc"][:, :4]
+    out = capi.Plan(buffer_size=n, mfcc_reference=True).extract(x, ["mfcc", "amplitudeSpectrum"])
+    exact = (out["amplitudeSpectrum"].view(np.uint32) == ref["amp"].view(np.uint32)).all(1)
+    assert exact.any()
+    g, r = out["mfcc"][exact], ref["mfcc"][exact]
+    same = (g.view(np.uint32) == r.view(np.uint32)) | (np.isnan(g) & np.isnan(r))
+    assert same.all(), (g[:, :4], r[:, :4])
