@@ -1009,14 +1009,16 @@ __device__ __forceinline__ void mel_reference_order(KArgs* ap, const float (&av)
 // put back after the chains. Per step: the conversion, product, sum and the two roundings on the
 // VALU; per group two 16-byte row loads, the 8 weights (shared by the track's F lanes), the next
 // control word and one LDS store.
-template <int N>
-__device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec* recs, float2* buf, bool pair, bool have_cur) {
+template <int N, bool PAIR>
+__device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec* recs, float2* buf, bool have_cur) {
+  constexpr bool pair = PAIR;
   constexpr int L = N / 2;
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) f32x4* GF4;
   static_assert(sizeof(FrameRec) == kRecBytes && offsetof(FrameRec, lm) == kRecLmOff, "chain_schedule's record offsets");
   const auto ctl = gbl(q->t.chain_ctl);
-  const int ng = q->chain_groups, F = pair ? 8 : 4;
+  constexpr int F = PAIR ? 8 : 4;
+  const int ng = q->chain_groups;
   const auto wp = gbl(q->t.chain_w) + (lane / F) * (ng * 8);
   unsigned char* const rb = reinterpret_cast<unsigned char*>(recs);
   float* const scratch = reinterpret_cast<float*>(buf) + lane;
@@ -1927,7 +1929,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         // wave's alone and the CU's L1 is coherent for its own waves (workgroup scope)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);
+        if (q->chain_pair) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);
+        else mel_chains<N, false>(q, opaque(lane), gbl(rows), recs, buf, true);
         wave_sync();  // the band energies are in the records: the log step reads them
       }
     }
@@ -2022,7 +2025,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       const int l2 = opaque(lane);
-      mel_chains<N>(q, l2, gbl(rows), recs, buf, true, false);
+      mel_chains<N, true>(q, l2, gbl(rows), recs, buf, false);
       wave_sync();
       mfcc_log<CHAIN, SUB>(q, l2, recs, 32);
       wave_sync();

@@ -17,15 +17,14 @@ PATCHES = {
     "no_phase2": [("    MGX_MARK(phase2_start);\n    prio_hi<4>();\n", "    MGX_MARK(phase2_start);\n    prio_hi<4>();\n    if (opaque(0)) {\n"),
                   ("    prio_lo<4>();\n    MGX_MARK(phase2_end);", "    }\n    prio_lo<4>();\n    MGX_MARK(phase2_end);")],
     "no_loud2": [("if (!LIGHT && q->need_spectrum && q->need_loudness) {", "if (opaque(0) && !LIGHT && q->need_spectrum && q->need_loudness) {")],
-    "no_ln": [("if (q->need_spectrum && q->need_mfcc) {\n        // mfcc.js:64",
-               "if (opaque(0) && q->need_spectrum && q->need_mfcc) {\n        // mfcc.js:64")],
-    "no_dct": [("if (q->need_spectrum && q->need_mfcc) {\n        const int nc",
-                "if (opaque(0) && q->need_spectrum && q->need_mfcc) {\n        const int nc")],
+    "no_ln": [("        mfcc_log<CHAIN, SUB>(q, l2, recs, 0);", "        if (opaque(0)) mfcc_log<CHAIN, SUB>(q, l2, recs, 0);")],
+    "no_dct": [("        mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 0, f0);",
+                "        if (opaque(0)) mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 0, f0);")],
     "no_scalars": [("for (int i = l2; i < (MGX_PERCEPTUAL_SHARPNESS + 1) * FPW; i += 64) {",
                     "for (int i = l2; opaque(0) && i < (MGX_PERCEPTUAL_SHARPNESS + 1) * FPW; i += 64) {")],
     # the frame samples from the address instead of HBM (is the frame load's latency exposed?)
-    "no_frame_load": [("float* p) { return *p; }",
-                       "float* p) { const uint32_t a = (uint32_t)(uintptr_t)p; return (float)((a >> 2) & 1023) * 0x1p-10f - 0.5f; }")],
+    "no_frame_load": [("  if constexpr (NT) return __builtin_nontemporal_load(p);\n  return *p;",
+                       "  const uint32_t a = (uint32_t)(uintptr_t)p; return (float)((a >> 2) & 1023) * 0x1p-10f - 0.5f;")],
     # the per-lane twiddle loads of passes >= 1 made lane-uniform scalar loads
     "twuni": [("""__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
   const GD q = (GD)p;""", """__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
@@ -44,16 +43,32 @@ PATCHES = {
                    "  const bool need_prefix = opaque(0);")],
     # MGX_FLAG_MFCC_REFERENCE (CHAIN kernels): the chains skipped (the occupancy / LDS-layout /
     # power-row cost alone)
-    "chain_none": [("        mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);",
-                    "        if (opaque(0)) mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);")],
+    "chain_none": [("        if (q->chain_pair) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);",
+                    "        if (opaque(0)) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);")],
+    # the chains' weight and row loads replaced by values from the control word (no loads)
+    "chain_noload": [("""#pragma unroll
+    for (int u = 0; u < 8; ++u) w[u] = wp[g * 8 + u];
+    const GF4 pr = (GF4)(ring + (c & 0x1FFFu));      // a multiple of 4 floats (chain_schedule)
+    const f32x4 p0 = pr[0], p1 = pr[1];""",
+                      """#pragma unroll
+    for (int u = 0; u < 8; ++u) w[u] = (double)(int)((c >> u) & 7u) * 0.125;
+    const f32x4 p0 = {(float)(c & 255u), (float)((c >> 3) & 255u), (float)((c >> 5) & 255u), (float)((c >> 7) & 255u)};
+    const f32x4 p1 = p0 * 0.5f;""")],
+    # the 8 steps of a chain group independent (summed by a tree): the dependency latency's share
+    "chain_nodep": [("""    acc = (double)(float)(a0 + w[0] * (double)p[0]);
+#pragma unroll
+    for (int u = 1; u < 8; ++u) acc = (double)(float)(acc + w[u] * (double)p[u]);  // two roundings, the float32 store""",
+                     """    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = (double)(float)((u ? (double)u : a0) + w[u] * (double)p[u]);
+    acc = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));""")],
     # the CHAIN kernels' power-row stores to the device-memory ring skipped (the chains read stale rows)
     "chain_norows": [("      for (int jj = 0; jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];",
                       "      for (int jj = 0; opaque(0) && jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];")],
     # the fence before the chains (a vmcnt(0) wait: the next frame's prefetch, the row stores) dropped
     "chain_nofence": [("""        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);""",
-                       """        mel_chains<N>(q, opaque(lane), gbl(rows), recs, buf, q->chain_pair, true);""")],
+        if (q->chain_pair)""", """        if (q->chain_pair)""")],
     # the FFT passes after pass 0 skipped (the exchanges too): what the f64 butterflies cost
     "no_passes": [("      if (tame) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);",
                    "      if (opaque(0)) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);"),
