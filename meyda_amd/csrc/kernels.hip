@@ -130,8 +130,10 @@ struct Geo {
   static constexpr bool BLIM_REG = N <= 512;
   static constexpr bool PREFETCH = PF != 0;
   // GROUP_SYNC: a workgroup barrier after every GROUP_SYNC-th full group of 16 frames, so the
-  // group's output lines are written together (extract_kernel; 0 = none)
-  static constexpr int GROUP_SYNC = N == 2048 ? 0 : 2;
+  // group's output lines are written together (extract_kernel; 0 = none). Measured per N
+  // (profiles/r03_group_sync.txt): 1024 +0.0 % (time-only -3.8 %), 256 -0.1 %; the all-feature
+  // launch at 512 +1.6 % and at 2048 (3 waves per SIMD) +2.3 %, so those keep none.
+  static constexpr int GROUP_SYNC = (N == 1024 || N == 256) ? 2 : 0;
   static constexpr bool LPREMAT = N == 2048;  // measured: N = 2048 1 % faster, N = 256 7 % slower
   static constexpr int MIX = 1;  // bfly_mixed_tame (form 0 was faster at N = 1024 at 128 live VGPRs)
   static_assert(R >= 2 && (R & (R - 1)) == 0, "N must be a power of two in [256, 2048]");
@@ -2011,7 +2013,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     // of a 64-byte scalar line was written back on its own: WRITE_SIZE 1.13x the outputs (time-only
     // set 1.40x). With the barrier: 1.016x (1.10x), all-feature launch +0.0 %, time-only -3.8 %,
     // outputs identical (profiles/r03_group_sync.txt). Every wave has a batch in a full group, so
-    // all four reach the same barriers. N = 2048 (3 waves per SIMD) lost 2.3 % and keeps none.
+    // all four reach the same barriers. N = 512 and 2048 lost 1.6 % and 2.3 % and keep none.
     if constexpr (G::GROUP_SYNC > 0) {
       const uint64_t g = (b - wave) / 4;
       if (g * 4 + 3 < nb && g % G::GROUP_SYNC == G::GROUP_SYNC - 1) __builtin_amdgcn_s_barrier();
