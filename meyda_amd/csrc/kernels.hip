@@ -937,58 +937,7 @@ __device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av
   }
 }
 
-// MGX_FLAG_MFCC_REFERENCE: the mel band energies in the reference's own order (mfcc.js:40-62).
-// Lane j < nfilt owns band j and walks its bins in ascending order: the weight
-// (k - b_j) / (b_{j+1} - b_j) on the rising segment, (b_{j+2} - k) / (b_{j+2} - b_{j+1}) on the
-// falling one, each the correctly rounded double quotient; the product with the float32 power
-// rounded to double; the sum rounded to double and stored to the Float32Array accumulator.
-// Bins outside [b_j, b_{j+2}) carry weight 0 in the reference and add exactly +0 there (finite
-// frames only; non-finite ones take nonfinite_frame_sums). The quotient t/d of two small
-// integers comes from r = 1/d (IEEE, once per segment) as q0 = t r, e = t - q0 d (exact by
-// FMA), q0 + e r: the correctly rounded quotient for every 0 <= t <= d <= 4096 (checked
-// exhaustively on the CPU; tests/test_capi_host.py), with no division in the loop.
-template <int N>
-__device__ __forceinline__ void mel_reference_order(KArgs* ap, const float (&av)[Geo<N>::R], int lane, float2* buf,
-                                                    FrameRec& rec) {
-  constexpr int R = Geo<N>::R;
-  double* prow = reinterpret_cast<double*>(buf);  // the frame's power spectrum, float32 values in double
-  wave_sync();  // band-sum reads of the prefix buffer are done
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj) prow[R * lane + jj] = (double)(av[jj] * av[jj]);  // powerSpectrum.js
-  wave_sync();
-  const int nf = ap->nfilt;
-  if (lane < nf) {
-    const auto b = gbl(ap->t.mel_bins);
-    constexpr int L = N / 2;  // the reference sums bins j < N/2 only
-    const int b0 = min(b[lane], L), b1 = min(b[lane + 1], L), b2 = min(b[lane + 2], L);
-    double acc = 0.0;  // the Float32Array element, held exactly in double
-    // One segment, 4 bins per step: the weights and products of a step are independent, only
-    // the accumulator is serial. Bins past the segment's end contribute an exact +0 (their
-    // product is selected away, never multiplied: the slot buffer holds other data there).
-    auto segment = [&](int k0, int k1, bool rising) {
-      if (k1 <= k0) return;
-      const double d = (double)(k1 - k0), r = 1.0 / d;
-      for (int k = k0; k < k1; k += 4) {
-        double pr[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const double t = (double)(rising ? k + u - k0 : k1 - k - u);
-          const double q0 = t * r;
-          const double w = __builtin_fma(__builtin_fma(-q0, d, t), r, q0);
-          const double p = prow[k + u];
-          pr[u] = k + u < k1 ? w * p : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc = (double)(float)(acc + pr[u]);  // two double roundings, the float32 store
-      }
-    };
-    segment(b0, b1, true);
-    segment(b1, b2, false);
-    rec.lm[lane] = (float)acc;
-  }
-}
-
-// MGX_FLAG_MFCC_REFERENCE at N <= 1024 (the CHAIN kernels): the mel band energies in the reference's
+// MGX_FLAG_MFCC_REFERENCE (the CHAIN kernels): the mel band energies in the reference's
 // own order (mfcc.js:53-62), over the power rows phase 1 left in the wave's ring in device memory
 // (KernelArgs::chain_rows). Each band of each frame is one serial chain: from its first bin in
 // ascending order, the weight (an IEEE double quotient, plan table) times the float32 power rounded
@@ -1489,8 +1438,6 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   if (nonfinite) {
     // (CHAIN with paired batches: the pair's first batch keeps its mel sums in the upper half of lm)
     nonfinite_frame_sums<N>(ap, av, lane, buf, rec, CHAIN && ap->chain_pair && !(it & 1) ? 32 : 0);
-  } else if (!CHAIN && SUB && ap->need_mfcc && ap->mfcc_reference) {  // (N = 2048 only; the all-feature kernel never has the flag)
-    mel_reference_order<N>(ap, av, lane, buf, rec);
   } else if (!CHAIN && ap->need_mfcc) {
     mel_energies<N>(ap, av, lane, buf, rec, mt);
   }
@@ -1661,7 +1608,7 @@ template <bool CHAIN, bool SUB>
 __device__ __forceinline__ void mfcc_log(KArgs* q, int l2, FrameRec* recs, int lmo) {
   constexpr int FPW = 4;
   const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
-  const bool ref_log = CHAIN || (SUB && q->mfcc_reference);  // the double Math.log, then float32
+  const bool ref_log = CHAIN;  // MGX_FLAG_MFCC_REFERENCE: the double Math.log, then float32
   auto ln1 = [&](float v, int band) {
     return band < nfilt ? (ref_log ? (float)log((double)v) : ln_f32(v)) : 0.0f;  // padding for dct_sum
   };
@@ -1679,10 +1626,10 @@ template <bool CHAIN, bool SUB>
 __device__ __forceinline__ void mfcc_dct(KArgs* q, int l2, FrameRec* recs, const float* dct_lds, int lmo, uint64_t fbase) {
   constexpr int FPW = 4;
   const int nc = q->ncoef, nfilt = q->nfilt;
-  if (q->dct_sequential || (SUB && !CHAIN && q->mfcc_reference)) {
-    // MGX_FLAG_DCT_SEQUENTIAL: VALU FMAs in the reference's sequential order, one lane per
-    // (coefficient, frame). (The matrix-core form below is the default: 0.5 % faster for the
-    // whole kernel and equal on every golden coefficient)
+  if (CHAIN || q->dct_sequential) {
+    // MGX_FLAG_DCT_SEQUENTIAL, and the reference-order MFCC (CHAIN): VALU FMAs in the reference's
+    // sequential order, one lane per (coefficient, frame). (The matrix-core form below is the
+    // default: 0.5 % faster for the whole kernel and equal on every golden coefficient)
     for (int i = l2; i < FPW * nc; i += 64) {
       const int c = i / FPW, fb = i % FPW;
       const uint64_t f = fbase + fb;
@@ -2119,7 +2066,7 @@ int occupancy_n(int ncoef, int nfilt) {
   return blocks;
 }
 
-// the instances a plan's launches use: MGX_FLAG_MFCC_REFERENCE at N <= 1024 takes the CHAIN pair
+// the instances a plan's launches use: MGX_FLAG_MFCC_REFERENCE takes the CHAIN pair
 // (all features / any subset), every other faithful plan the four below
 template <int N>
 constexpr bool kChainN = N <= kChainMaxN;
@@ -2157,16 +2104,15 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
     }
   }
   // a spectral feature subset that skips the moment / prefix / time-domain work takes the SUB kernel
-  // (and so does MGX_FLAG_MFCC_REFERENCE at N = 2048: mel_reference_order, one frame at a time)
   // (LIGHT: a subset reading neither the moments nor the prefix row, e.g. mfcc or the spectra
   // alone, compiled without that code: no runtime branches to keep its registers live)
-  if (a.need_spectrum && a.need_mom == 0 && !a.need_prefix && !a.mfcc_reference)
+  if (a.need_spectrum && a.need_mom == 0 && !a.need_prefix)
     return launch_n<N, true, false, true, true>(a, grid, stream);
   // (NOTIME: every spectral sum but no rms / energy / zcr, e.g. C3: the all-feature schedule
   // with the time-domain reductions compiled out)
-  if (a.need_spectrum && a.need_mom == 2 && a.need_prefix && !a.need_energy && !a.need_zcr && !a.mfcc_reference)
+  if (a.need_spectrum && a.need_mom == 2 && a.need_prefix && !a.need_energy && !a.need_zcr)
     return launch_n<N, true, false, false, false, true>(a, grid, stream);
-  if (a.need_spectrum && (!every || a.mfcc_reference))
+  if (a.need_spectrum && !every)
     return launch_n<N, true, false, true>(a, grid, stream);
   return launch_n<N, true, false>(a, grid, stream);
 }

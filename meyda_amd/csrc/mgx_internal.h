@@ -12,12 +12,12 @@ constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
 constexpr int kMelHead = kMaxMel + 2;  // mel scratch: segment sums [0, nfilt + 2), head partials from here
-// Mel band chains in the reference's own order (MGX_FLAG_MFCC_REFERENCE, N <= 1024): F frames x
+// Mel band chains in the reference's own order (MGX_FLAG_MFCC_REFERENCE, every N): F frames x
 // nfilt chains on 64 / F packed tracks (F = 8 for nfilt <= 31, else F = 4; plan.cpp chain_schedule).
 constexpr int kRecBytes = 520;  // sizeof(FrameRec) (kernels.hip)
 constexpr int kRecLmOff = 248;  // offsetof(FrameRec, lm)
 constexpr int kChainPairMaxMel = 31;  // paired batches keep two halves of FrameRec::lm (flag at 31)
-constexpr int kChainMaxN = 1024;
+constexpr int kChainMaxN = 2048;
 constexpr int kChainSkip = 1 << 30;  // FrameRec.zcr flag bit: a non-finite frame keeps its phase-1 mel sums
 // dwords of one lane's mel record for R bins per lane (R weights, R slot bytes, R keep bytes,
 // 8 bytes of scan keeps and slots), padded to whole 16-byte loads
@@ -33,7 +33,7 @@ struct DevTables {
   const uint32_t* mel_rec;   // 64 per-lane records of the mel segment tables (plan.cpp mel_lane_tables)
   const int* mel_bins;       // nfilt + 2 filter edges (mfcc.js:15-38), for the non-finite-frame path
   const float* dct;          // ncoef * nfilt, dct[c + j*ncoef] (mfcc.js:67-83)
-  // MGX_FLAG_MFCC_REFERENCE at N <= 1024 (plan.cpp chain_schedule, kernels.hip mel_chains):
+  // MGX_FLAG_MFCC_REFERENCE (plan.cpp chain_schedule, kernels.hip mel_chains):
   const uint32_t* chain_ctl; // per 8-step group and lane: row offset, chain start, the finished chain's store
   const double* chain_w;     // per track, the weights of its chains' steps back to back
 };
@@ -60,7 +60,6 @@ struct KernelArgs {
   int need_energy;       // rms or energy: the wave sum of the squares (SUB kernel)
   int need_zcr;          // zcr: the sign-change ballots (SUB kernel)
   int dct_sequential;    // MGX_FLAG_DCT_SEQUENTIAL: the DCT as VALU FMAs in the reference's order
-  int mfcc_reference;    // MGX_FLAG_MFCC_REFERENCE: mel sums, log and DCT in the reference's order (SUB kernel)
   int mel_zero;          // some mel segment [b_m, b_{m+1}) is empty: the scan's slots are zeroed first
   int wg_ranks;          // workgroups per CU when the grid is the resident one (else 1): their work shares
   int chain_groups;      // 8-step groups of the mel chain tracks (0: the segmented scan)

@@ -285,7 +285,7 @@ void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& 
   }
 }
 
-// MGX_FLAG_MFCC_REFERENCE at N <= 1024: the mel band sums of mfcc.js:53-62 in the reference's
+// MGX_FLAG_MFCC_REFERENCE: the mel band sums of mfcc.js:53-62 in the reference's
 // own order, as serial chains (kernels.hip mel_chains). Band j's chain walks its bins
 // [b_j, b_{j+2}) (clamped to the reference's j < N/2) in ascending order with the weights of
 // mfcc.js:43-50 -- (k - b_j) / (b_{j+1} - b_j) rising, (b_{j+2} - k) / (b_{j+2} - b_{j+1}) falling,
@@ -410,7 +410,7 @@ struct mgx_plan {
   int grid_cap = 1;
   int cus = 0;  // compute units of the plan's device
   int mel_zero = 1;  // some mel segment is empty (kernels.hip mel_energies)
-  int chain_groups = 0;  // MGX_FLAG_MFCC_REFERENCE at N <= 1024: 8-step groups of the mel chains (chain_schedule)
+  int chain_groups = 0;  // MGX_FLAG_MFCC_REFERENCE: 8-step groups of the mel chains (chain_schedule)
   int chain_pair = 0;  // ... over two consecutive batches of a wave (8 frames)
   // the mel chains' power-row rings (kernels.hip KGeo::GROWS), one per stream a launch used: the
   // launches of one stream run in order, those of two streams may overlap
@@ -652,7 +652,6 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.ncoef = (int)p->d.num_mfcc_coeffs;
   a.scalar_f64 = (int)p->d.scalar_f64;
   a.dct_sequential = (p->d.flags & MGX_FLAG_DCT_SEQUENTIAL) ? 1 : 0;
-  a.mfcc_reference = (p->d.flags & MGX_FLAG_MFCC_REFERENCE) ? 1 : 0;
   a.mel_zero = p->mel_zero;
   a.chain_groups = p->chain_groups;
   a.chain_pair = p->chain_pair;

@@ -15,7 +15,7 @@ from test_gpu_parity import _mfcc_reference_checks
 
 pytestmark = pytest.mark.gpu
 
-CHAIN_SIZES = [256, 512, 1024]
+CHAIN_SIZES = [256, 512, 1024, 2048]
 
 
 @pytest.fixture(scope="module")
