@@ -312,6 +312,9 @@ struct ChainSched {
   std::vector<uint32_t> ctl;
   std::vector<double> w;
 };
+// (the control word's fields hold every plan: 8 frames' rows at N = kChainMaxN, the last record's lm[63])
+static_assert(8 * (mgx::kChainMaxN / 2) - 1 <= 0x1FFF, "row offsets fit bits 0-12");
+static_assert(3 * mgx::kRecBytes + mgx::kRecLmOff + 4 * (mgx::kMaxMel - 1) <= 0xFFF, "record offsets fit bits 13-24");
 void chain_schedule(const int32_t* b, int nf, int L, int F, ChainSched& cs) {
   const int ntr = 64 / F;
   std::vector<int> lo(nf), len(nf), order;
