@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: time the shards alone, without the RCCL gather to rank 0")
     ap.add_argument("--chunks", type=int, default=0, help="N > 1: gather pipeline depth (0 = automatic)")
-    ap.add_argument("--gather-timeout", type=float, default=180.0,
+    ap.add_argument("--gather-timeout", type=float, default=60.0,
                     help="N > 1: deadline (s) of the gather phase; past it rank 0 reports the shards alone")
     ap.add_argument("--allow-shared-gpu", action="store_true",
                     help="rehearsal only: ranks may share a GPU (RCCL refuses that, so no gather)")
