@@ -142,3 +142,21 @@ def test_gather_protocol_world2_matches_single_process(total, nch):
     for p in procs:
         p.join(timeout=60)
     assert sorted(res, key=lambda t: t[1]) == [("ok", 0), ("ok", 1)], res
+
+
+def test_bench_value_is_the_shards_rate():
+    """The path partitions (independent frames): at N > 1 the line's value is the shards' rate;
+    the RCCL gather-inclusive rate of the same run is reported beside it, never as value."""
+    import types
+
+    import bench
+    args = types.SimpleNamespace(steps=10, warmup=2, precision="faithful", single_stream=False)
+    st = {"launch_alone_mean_ms": 0.6}
+    line = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, st,
+                            {"status": "ok", "value": 2.8e9}, {})
+    assert line["value"] == 3.5e9 and line["n_gpus"] == 8 and line["scaling"] == "weak"
+    assert line["gather"]["value"] == 2.8e9 and abs(line["gather"]["vs_shards"] - 0.8) < 1e-12
+    assert line["config"]["gather_to_rank0"] is True
+    failed = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, st,
+                              {"status": "failed on rank 3"}, {})
+    assert failed["value"] == 3.5e9 and failed["config"]["gather_to_rank0"] is False
