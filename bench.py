@@ -27,6 +27,15 @@ gather's status if it fails or passes its deadline. (Rank 0's inbound xGMI bound
 7 peers x 52 MB of records per 262,144-frame step.) The RCCL communicator's own view (ranks, rank, device) and every
 rank's GPU (uuid, PCI bus) are in the line. torch.distributed (gloo) is only the control
 plane: the RCCL id broadcast, barriers and the max-over-ranks elapsed time.
+
+Config C5 (BASELINE.json configs[4]: bufferSize=2048, all features incl. MFCC, 262,144
+frames per GPU -- 2,097,152 at 8 GPUs -- with the RCCL gather) is the `c5` field of every
+line: its shards' rate, and at N > 1 its gather-inclusive rate, `vs_shards` and the
+communicator's view (at N = 1 the gather is reported as skipped).
+
+A gather that fails or passes its deadline leaves `value` (the shards) measured: rank 0
+still prints the line with the gather's status and the process exits 0, unless
+--strict-gather asks for exit status 3 in that case.
 """
 import argparse
 import concurrent.futures as cf
@@ -46,9 +55,11 @@ from meyda_amd import capi  # noqa: E402
 FEATURES = capi.ALL_FEATURES  # 13 scalars + loudness.specific(24) + mfcc(13)
 OUT_FLOATS = 3 + 7 + 25 + 2 + 13  # per frame, f32 outputs
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+C5_N = 2048  # BASELINE.json configs[4]
+C3_FEATURES = [f for f in FEATURES if f not in ("rms", "energy", "zcr", "mfcc")]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs of the job (default: the torchrun world size, else 1). Under torchrun it must equal "
@@ -67,22 +78,32 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer measurement")
     ap.add_argument("--cpu-seconds", type=float, default=6.0,
-                    help="CPU baseline: seconds of the multi-thread run (1 thread and the C port: a third)")
+                    help="CPU baseline: seconds of the multi-thread run of the headline set (1 thread and the C "
+                         "port: a third; each other config: half)")
     ap.add_argument("--no-fast", action="store_true", help="N = 1: skip the fp32-butterfly mode beside the faithful one")
     ap.add_argument("--no-c3", action="store_true", help="N = 1: skip the config C3 feature set (spectral* + loudness)")
+    ap.add_argument("--no-c2", action="store_true", help="N = 1: skip config C2 (N = 512, amplitude + centroid)")
     ap.add_argument("--no-c4", action="store_true", help="N = 1: skip config C4 exactly (40 mel bands, 13 MFCC)")
+    ap.add_argument("--no-c5", action="store_true", help="skip config C5 (bufferSize 2048, all features, + gather)")
+    ap.add_argument("--c5-frames", type=int, default=262144, help="C5 frames per GPU per step")
+    ap.add_argument("--no-mfcc-exact", action="store_true",
+                    help="N = 1: skip the reference-order MFCC (MGX_FLAG_MFCC_REFERENCE) timing")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="N = 1: skip the per-call get() / streaming latency of the JS facade (node)")
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: time the shards alone, without the RCCL gather to rank 0")
     ap.add_argument("--chunks", type=int, default=0, help="N > 1: gather pipeline depth (0 = automatic)")
     ap.add_argument("--gather-timeout", type=float, default=60.0,
-                    help="N > 1: deadline (s) of the gather phase; past it rank 0 reports the shards alone")
+                    help="N > 1: deadline (s) of each gather phase; past it rank 0 reports the shards alone")
+    ap.add_argument("--strict-gather", action="store_true",
+                    help="N > 1: exit status 3 (after the line is printed) when a gather failed or timed out")
     ap.add_argument("--allow-shared-gpu", action="store_true",
                     help="rehearsal only: ranks may share a GPU (RCCL refuses that, so no gather)")
     ap.add_argument("--no-every-output", action="store_true",
                     help="N = 1: skip the secondary timing with every output (spectra too) and 40 mel bands")
     ap.add_argument("--no-pmc", action="store_true",
                     help="N = 1: skip the live rocprofv3 --pmc passes (HBM traffic, VALU instruction mix)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 CPU_THREADS = 16  # the GPU box's CPU share per GPU (os.cpu_count() there is the whole machine)
@@ -110,34 +131,85 @@ def cpu_port_c(n, seconds, threads):
     return {"value": sum(r[0] for r in res) / wall, "unit": "frames/s", "cores": threads, "kind": "port-c"}
 
 
+# The CPU baseline of every GPU config ("on the same seeded synthetic batches and
+# feature sets as each GPU config"): oracle/js/bench_cpu.js feature sets
+CPU_SETS = {"c2": (512, "c2", "amplitudeSpectrum + spectralCentroid"),
+            "c3": (1024, "c3", "spectral* + loudness + perceptual"),
+            "c4": (1024, "c4", "40-band mel + 13 MFCC"),
+            "c5": (C5_N, "all", "all features incl. 26-band MFCC")}
+
+
+def node_cpu(n, seconds, threads, fset="all", timeout_extra=120):
+    import subprocess
+    js = os.path.join(ROOT, "oracle", "js", "bench_cpu.js")
+    r = subprocess.run(["node", js, str(n), str(seconds), str(threads), "reference", fset], capture_output=True,
+                       text=True, timeout=timeout_extra + 4 * seconds, check=True)
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def cpu_baseline(n, seconds):
     """The reference's Node/jsfft CPU path as the build's JavaScript restatement
     (oracle/js/meyda_cpu.js, bit-exact to the reference's golden outputs), in the
     reference's per-buffer structure, timed on this host with 1 and CPU_THREADS
-    worker_threads on the seeded stream; the C port beside it."""
+    worker_threads on the seeded stream; the C port beside it. The
+    other configs' feature sets ride along in `configs` (C1 as µs per get() call)."""
     import shutil
-    import subprocess
     threads = min(CPU_THREADS, os.cpu_count() or 1)
-    js = os.path.join(ROOT, "oracle", "js", "bench_cpu.js")
     out = {"unit": "frames/s", "kind": "js-restatement"}
     if shutil.which("node"):
-        def run(t, secs):
-            r = subprocess.run(["node", js, str(n), str(secs), str(t), "reference"], capture_output=True, text=True,
-                               timeout=120 + 4 * secs, check=True)
-            return json.loads(r.stdout.strip().splitlines()[-1])
-        one = run(1, max(1.0, seconds / 3))
-        many = run(threads, seconds)
+        one = node_cpu(n, max(1.0, seconds / 3), 1)
+        many = node_cpu(n, seconds, threads)
         out.update({"value": many["value"], "cores": threads, "cpu_model": many["cpu_model"],
                     "logical_cpus": many["logical_cpus"], "node": many["node"], "one_thread": one["value"],
                     "sample": "%d frames (N=%d, all features, seeded noise, the reference's per-buffer structure) "
                               "over %.1f s on %d worker_threads; 1 thread: %.0f frames/s"
                               % (many["frames"], n, many["seconds"], threads, one["value"])})
+        cfgs = {}
+        for key, (cn, fset, what) in CPU_SETS.items():
+            try:
+                m = node_cpu(cn, max(1.0, seconds / 2), threads, fset)
+                o = node_cpu(cn, max(0.5, seconds / 6), 1, fset)
+                cfgs[key] = {"value": m["value"], "unit": "frames/s", "cores": threads, "one_thread": o["value"],
+                             "kind": "js-restatement",
+                             "sample": "%d frames (N=%d, %s, seeded noise) over %.1f s on %d worker_threads"
+                                       % (m["frames"], cn, what, m["seconds"], threads)}
+            except Exception as e:  # a report, never the measurement itself
+                cfgs[key] = {"value": None, "note": "failed: %r" % (e,)}
+        try:
+            c1 = node_cpu(512, 2.0, 1, "c1")
+            cfgs["c1"] = {"value": c1["us_per_call"], "unit": "us per get(['rms','spectralCentroid']) call",
+                          "calls": c1["calls"], "cores": 1, "kind": "js-restatement",
+                          "sample": "sound1.wav frame 0 (tests/golden, N=512): window, FFT, amplitude, rms and "
+                                    "centroid per call, median of %d calls" % c1["calls"]}
+        except Exception as e:
+            cfgs["c1"] = {"value": None, "note": "failed: %r" % (e,)}
+        out["configs"] = cfgs
     else:  # no Node on this host: the C port stands in
         out.update({"kind": "port", "value": None, "note": "node not found"})
     out["port_c"] = cpu_port_c(n, max(1.0, seconds / 3), threads)
     if out.get("value") is None:
         out["value"] = out["port_c"]["value"]
         out["cores"] = threads
+    return out
+
+
+def latency_js():
+    """The real-time path through the product's own JS facade over the N-API addon
+    (tools/latency.js): C1's get(['rms','spectralCentroid']) per call, and the start() /
+    process() callback path at batchFrames 1 and 64. A report; never `value`."""
+    import shutil
+    import subprocess
+    addon = os.path.join(ROOT, "meyda_amd", "addon", "meyda_napi.node")
+    if not shutil.which("node"):
+        return {"status": "skipped (node not found)"}
+    if not os.path.exists(addon):
+        return {"status": "skipped (meyda_amd/addon/meyda_napi.node not built)"}
+    r = subprocess.run(["node", os.path.join(ROOT, "tools", "latency.js")], capture_output=True, text=True,
+                       timeout=240)
+    if r.returncode != 0:
+        return {"status": "failed (rc %d): %s" % (r.returncode, r.stderr.strip()[-400:])}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["status"] = "ok"
     return out
 
 
@@ -166,6 +238,25 @@ class Devices:
     def sync(self):
         for d in self.devs:
             torch.cuda.synchronize(d)
+
+
+class Workload:
+    """One configuration's synthetic frames (each local device its own shard of one global
+    stream, generated in HBM) and a plan per device."""
+
+    def __init__(self, n, F, devs, first, precision):
+        self.n, self.F = n, F
+        self.frames, self.plans = {}, {}
+        for i, d in enumerate(devs.devs):
+            with torch.cuda.device(d):
+                self.frames[d] = torch.empty(F, n, dtype=torch.float32, device="cuda:%d" % d)
+                capi.synth_frames_device(self.frames[d], capi_seed(), first_frame=(first + i) * F)
+                self.plans[d] = capi.Plan(buffer_size=n, precision=precision, device=d)
+
+    def close(self):
+        for p in self.plans.values():
+            p.close()
+        self.frames, self.plans = {}, {}
 
 
 def pipelined(step, devs, first, count):
@@ -217,6 +308,12 @@ def host_path(plan, frames, reps=3):
             "note": "PCIe-inclusive: %d float32 frames from pageable host memory, features back to host" % x.shape[0]}
 
 
+def _mfma_pass(c):
+    # the DCT's v_mfma_f64_4x4x4_4b_f64: 4 blocks x 4x4x4 = 256 FMAs = 512 FLOP per wave instruction
+    return {"instr_per_launch": c["SQ_INSTS_VALU_MFMA_F64"], "flop_per_launch": 512 * c["SQ_INSTS_VALU_MFMA_F64"],
+            "busy_cycles_per_launch": c["SQ_VALU_MFMA_BUSY_CYCLES"], "gui_active_cycles": c["GRBM_GUI_ACTIVE"]}
+
+
 def pmc_live(n, F, precision):
     """Counters of the same workload, measured in this run: rocprofv3 --pmc passes (one
     counter block each, kernel-trace only, MI355X_MICROARCH.md HBM section) over
@@ -233,16 +330,20 @@ def pmc_live(n, F, precision):
         return None, None, "rocprofv3 not found"
     probe = os.path.join(ROOT, "tools", "pmc_probe.py")
     tmp = tempfile.mkdtemp(prefix="mgx_pmc_", dir="/tmp")
-    passes = {"fetch_t": ("time_only", "FETCH_SIZE"), "fetch": ("all", "FETCH_SIZE"), "write": ("all", "WRITE_SIZE"),
-              "valu": ("all", "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 "
-                              "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS"),
-              "mfma": ("all", "SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES "
-                              "GRBM_GUI_ACTIVE")}
+    mfma = "SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+    passes = {"fetch_t": ("time_only", 26, "FETCH_SIZE"), "fetch": ("all", 26, "FETCH_SIZE"),
+              "write": ("all", 26, "WRITE_SIZE"),
+              "valu": ("all", 26, "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 "
+                                  "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS"),
+              "mfma": ("all", 26, mfma),
+              # config C4 exactly (40 mel bands, mfcc alone): north_star's MFMA utilisation of that line
+              "mfma_c4": ("mfcc", 40, mfma)}
     got = {}
     reps = 3
-    for key, (fset, ctrs) in passes.items():
+    for key, (fset, bands, ctrs) in passes.items():
         d = os.path.join(tmp, key)
-        env = dict(os.environ, PROBE_SET=fset, PROBE_N=str(n), PROBE_PREC=precision, PROBE_REPS=str(reps), TMPDIR="/tmp")
+        env = dict(os.environ, PROBE_SET=fset, PROBE_N=str(n), PROBE_PREC=precision, PROBE_REPS=str(reps),
+                   PROBE_BANDS=str(bands), TMPDIR="/tmp")
         cmd = ["timeout", "-s", "KILL", "90", prof, "--pmc", *ctrs.split(), "--kernel-trace", "--output-format", "csv",
                "-d", d, "-o", "run", "--", sys.executable, probe]
         r = subprocess.run(cmd, env=env, cwd="/tmp", capture_output=True, text=True)
@@ -265,10 +366,8 @@ def pmc_live(n, F, precision):
             "f64_per_frame": sum(v[k] for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
                                                 "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")) / F,
             "lds_per_frame": v["SQ_INSTS_LDS"] / F}
-    mm = got["mfma"]
-    # the DCT's v_mfma_f64_4x4x4_4b_f64: 4 blocks x 4x4x4 = 256 FMAs = 512 FLOP per wave instruction
-    valu["mfma_f64"] = {"instr_per_launch": mm["SQ_INSTS_VALU_MFMA_F64"], "flop_per_launch": 512 * mm["SQ_INSTS_VALU_MFMA_F64"],
-                        "busy_cycles_per_launch": mm["SQ_VALU_MFMA_BUSY_CYCLES"], "gui_active_cycles": mm["GRBM_GUI_ACTIVE"]}
+    valu["mfma_f64"] = _mfma_pass(got["mfma"])
+    valu["mfma_f64_c4"] = dict(_mfma_pass(got["mfma_c4"]), config="C4: 40 mel bands x 13 MFCC, mfcc alone")
     note = ("live: rocprofv3 --pmc passes of this run over tools/pmc_probe.py (%d frames x N=%d, same features); "
             "FETCH_SIZE x %.4f (time-only calibration), reads %.4g B + writes %.4g B per launch" % (F, n, cal, read, write))
     return read + write, valu, note
@@ -321,6 +420,60 @@ def run_mode(step, devs, steps, warmup, dist):
     return elapsed, period, stats
 
 
+def measure_shards(wl, devs, args, dist, feats=FEATURES):
+    """The shards alone: every local device extracts its own shard (no data-path collective)."""
+    sets = {d: [wl.plans[d].alloc_outputs(wl.F, feats, device="cuda:%d" % d) for _ in range(2)] for d in devs.devs}
+
+    def step(k):
+        for d in devs.devs:
+            wl.plans[d].extract_device(wl.frames[d].data_ptr(), wl.F, sets[d][k & 1][1], devs.stream(d, k).cuda_stream)
+    devs.sync()
+    settle(step, devs, args.settle_ms, dist)
+    return run_mode(step, devs, args.steps, args.warmup, dist)
+
+
+def measure_gather(wl, devs, args, dist, mode, rank, world, gpus, out):
+    """The same steps through the library's multi-device group: each rank's feature records
+    gathered to rank 0 over RCCL inside every step (group.cpp). Updates `out` as it goes (the
+    communicator's view, then the status and rates) so a deadline can report what it got."""
+    d0 = devs.devs[0]
+    n, F = wl.n, wl.F
+    out["status"] = "creating the group"
+    if mode == "torchrun":
+        uid = [capi.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        group = capi.Group(buffer_size=n, rank=rank, nranks=world, unique_id=uid[0], precision=args.precision, device=d0)
+    else:
+        group = capi.Group(buffer_size=n, devices=devs.devs, precision=args.precision)
+    comm = group.comm_info()
+    out["rccl_comm"] = {"ranks": comm[0], "rank": comm[1], "device": comm[2], "group_ranks": group.nranks,
+                        "local_ranks": group.num_local}
+    if group.nranks != gpus or comm[0] != gpus or comm[2] != d0 or comm[1] != group.first_local:
+        raise RuntimeError("the RCCL communicator reports %s for a %d-GPU job on device %d" % (comm, gpus, d0))
+    out["status"] = "running"
+    # rank 0 holds the whole job's feature record; the other ranks only their transfer buffers
+    # (two output sets: consecutive steps are in flight together, pipelined())
+    root = group.first_local == 0
+    plan = wl.plans[d0]
+    with torch.cuda.device(d0):
+        sets = [plan.alloc_outputs(F * gpus if root else 1, FEATURES, device="cuda:%d" % d0) for _ in range(2)]
+    mask = capi.output_mask(sets[0][1])
+    ptrs = [wl.frames[d].data_ptr() for d in devs.devs]
+
+    def step_gather(k):
+        group.extract_device(ptrs, [F] * gpus, sets[k & 1][1] if root else None, mask, args.chunks,
+                             [devs.stream(d, k).cuda_stream for d in devs.devs])
+    settle(step_gather, devs, args.settle_ms, dist)
+    el_g, km_g, stats_g = run_mode(step_gather, devs, args.steps, args.warmup, dist)
+    if root:  # spot check: the gathered record holds every rank's shard (last frame of each)
+        chk = sets[0][0]["zcr"].view(gpus, F)[:, -1]
+        out["finite_last_frames"] = bool(torch.all((chk >= 0) & (chk < n)).item())
+    out.update({"status": "ok", "value": gpus * F * args.steps / el_g, "ms_per_step": el_g / args.steps * 1e3,
+                "kernel_ms": km_g, "step_event_ms": stats_g})
+    devs.sync()
+    group.close()
+
+
 def resolve_topology(gpus, env, ndev, allow_shared=False):
     """How this run maps onto GPUs; fails loudly (SystemExit) instead of measuring fewer GPUs
     than asked. Under torchrun (WORLD_SIZE set) --gpus must equal the world size and every
@@ -347,15 +500,16 @@ def resolve_topology(gpus, env, ndev, allow_shared=False):
 
 
 class Watchdog:
-    """Deadline of the gather phase of a multi-GPU run. The RCCL path cannot be interrupted
+    """Deadline of one gather phase of a multi-GPU run. The RCCL path cannot be interrupted
     once a peer is missing (a rank that failed, a message never posted), so when the deadline
     passes rank 0 prints the line it already has -- the shards measured without the gather,
-    with the gather's status -- and every rank leaves (exit 0, so the launcher does not tear
-    rank 0 down before it has printed)."""
+    with the gather's status -- and every rank leaves (exit_code(): 0 unless --strict-gather,
+    so the launcher does not tear rank 0 down before it has printed)."""
 
-    def __init__(self, seconds, emit):
+    def __init__(self, seconds, emit, code):
         import threading
         self.emit = emit
+        self.code = code
         self.t = threading.Timer(seconds, self._fire)
         self.t.daemon = True
         self.t.start()
@@ -366,10 +520,38 @@ class Watchdog:
         finally:
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(0)
+            os._exit(self.code)
 
     def cancel(self):
         self.t.cancel()
+
+
+def shard_fields(gpus, F, n, el, km, stats, steps, bytes_per_frame):
+    """Rate and roofline of one config's shards (rank 0's launch duration)."""
+    alone = (stats["rank0"] if "rank0" in stats else stats)["launch_alone_mean_ms"]
+    return {"value": gpus * F * steps / el, "unit": "frames/s", "ms_per_step": el / steps * 1e3,
+            "kernel_ms": alone, "period_ms": km, "bytes_per_frame": bytes_per_frame,
+            "roofline_frac": F * bytes_per_frame / (alone * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frac_pipelined": F * bytes_per_frame / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, "step_event_ms": stats}
+
+
+def c5_field(gpus, F5, el, km, stats, steps, gather_on, chunks=0):
+    """The `c5` field of the line (BASELINE.json configs[4]) from its shards' timing; its gather
+    entry starts as "not run" at N > 1 (measure_gather fills it) and says why it is absent at
+    N = 1."""
+    c5 = dict(shard_fields(gpus, F5, C5_N, el, km, stats, steps, 4 * C5_N + 4 * OUT_FLOATS),
+              buffer_size=C5_N, frames_per_gpu=F5, features=FEATURES, mel_bands=26, mfcc_coeffs=13,
+              frames_total=gpus * F5,
+              workload="C5: %d frames x bufferSize=%d per GPU (%d in all; BASELINE's 2,097,152 at 8 GPUs), every "
+                       "feature incl. MFCC, frames sharded, records gathered to rank 0 over RCCL"
+                       % (F5, C5_N, gpus * F5))
+    if gather_on:
+        c5["gather"] = {"status": "not run", "chunks": chunks or "auto"}
+    elif gpus == 1:
+        c5["gather"] = {"status": "skipped (1 GPU): nothing to gather; the RCCL path is timed at N > 1"}
+    else:
+        c5["gather"] = {"status": "off (--no-gather or shared GPUs)"}
+    return c5
 
 
 def main():
@@ -399,84 +581,55 @@ def main():
     if shared and not args.allow_shared_gpu:
         raise SystemExit("bench.py: ranks share a GPU: %s" % placement)
     n, F = args.n, args.frames
-    # each rank / device its own shard of one global synthetic stream
-    first = rank if dist else 0
-    frames, plans = {}, {}
-    for i, d in enumerate(devs.devs):
-        with torch.cuda.device(d):
-            frames[d] = torch.empty(F, n, dtype=torch.float32, device="cuda:%d" % d)
-            capi.synth_frames_device(frames[d], capi_seed(), first_frame=(first + i) * F)
-            plans[d] = capi.Plan(buffer_size=n, precision=args.precision, device=d)
-    plan, d0 = plans[devs.devs[0]], devs.devs[0]
-    # the shards alone: every local device extracts its own shard (no data-path collective)
-    shard_sets = {d: [plans[d].alloc_outputs(F, FEATURES, device="cuda:%d" % d) for _ in range(2)] for d in devs.devs}
-
-    def step_shards(k):
-        for d in devs.devs:
-            plans[d].extract_device(frames[d].data_ptr(), F, shard_sets[d][k & 1][1], devs.stream(d, k).cuda_stream)
-    devs.sync()
-    settle(step_shards, devs, args.settle_ms, dist)
-    el_s, km_s, stats_s = run_mode(step_shards, devs, args.steps, args.warmup, dist)
+    first = rank if dist else 0  # each rank / device its own shard of one global synthetic stream
+    gather_on = gpus > 1 and not args.no_gather and not shared
+    head = Workload(n, F, devs, first, args.precision)
+    el_s, km_s, stats_s = measure_shards(head, devs, args, dist)
     value_s = gpus * F * args.steps / el_s
-    gather = None
-    if gpus > 1 and not args.no_gather and not shared:
-        gather = {"status": "not run", "chunks": args.chunks or "auto"}
+    gather = {"status": "not run", "chunks": args.chunks or "auto"} if gather_on else None
     line_box = {}
+    failed = []
 
-    def emit_line(gather_status=None):
+    # C5 (BASELINE configs[4]): the shards first (no collective), its gather after the headline's
+    c5 = None
+    if not args.no_c5:
+        w5 = Workload(C5_N, args.c5_frames, devs, first, args.precision)
+        el5, km5, st5 = measure_shards(w5, devs, args, dist)
+        c5 = c5_field(gpus, args.c5_frames, el5, km5, st5, args.steps, gather_on, args.chunks)
+        line_box["c5"] = c5
+    if mode == "one":
+        line_box.update(secondary(args, head.plans[devs.devs[0]], head.frames[devs.devs[0]], devs, n, F))
+
+    def emit_line(gather_status=None, target=None):
         """Rank 0's JSON line from what has been measured so far."""
         if rank != 0:
             return
-        if gather is not None and gather_status is not None:
-            gather["status"] = gather_status
+        if target is not None and gather_status is not None:
+            target["status"] = gather_status
         print(json.dumps(build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, gather,
                                     line_box)), flush=True)
 
-    if gather is not None:
-        wd = Watchdog(args.gather_timeout, emit_line)
+    code = 3 if args.strict_gather else 0
+    phases = []
+    if gather_on:
+        phases.append((head, gather))
+        if c5 is not None:
+            phases.append((w5, c5["gather"]))
+    for wl, target in phases:
+        wd = Watchdog(args.gather_timeout, lambda s, t=target: emit_line(s, t), code)
         try:
-            if mode == "torchrun":
-                uid = [capi.comm_unique_id() if rank == 0 else None]
-                dist.broadcast_object_list(uid, src=0)
-                group = capi.Group(buffer_size=n, rank=rank, nranks=world, unique_id=uid[0], precision=args.precision,
-                                   device=d0)
-            else:
-                group = capi.Group(buffer_size=n, devices=devs.devs, precision=args.precision)
-            comm = group.comm_info()
-            gather["rccl_comm"] = {"ranks": comm[0], "rank": comm[1], "device": comm[2], "group_ranks": group.nranks,
-                                   "local_ranks": group.num_local}
-            if group.nranks != gpus or comm[0] != gpus or comm[2] != d0 or comm[1] != group.first_local:
-                raise RuntimeError("the RCCL communicator reports %s for a %d-GPU job on device %d" % (comm, gpus, d0))
-            # rank 0 holds the whole job's feature record; the other ranks only their transfer
-            # buffers (two output sets: consecutive steps are in flight together, pipelined())
-            root = group.first_local == 0
-            with torch.cuda.device(d0):
-                sets = [plan.alloc_outputs(F * gpus if root else 1, FEATURES, device="cuda:%d" % d0) for _ in range(2)]
-            mask = capi.output_mask(sets[0][1])
-            ptrs = [frames[d].data_ptr() for d in devs.devs]
-
-            def step_gather(k):
-                group.extract_device(ptrs, [F] * gpus, sets[k & 1][1] if root else None, mask, args.chunks,
-                                     [devs.stream(d, k).cuda_stream for d in devs.devs])
-            settle(step_gather, devs, args.settle_ms, dist)
-            el_g, km_g, stats_g = run_mode(step_gather, devs, args.steps, args.warmup, dist)
-            if root:  # spot check: the gathered record holds every rank's shard (last frame of each)
-                chk = sets[0][0]["zcr"].view(gpus, F)[:, -1]
-                gather["finite_last_frames"] = bool(torch.all((chk >= 0) & (chk < n)).item())
-            gather.update({"status": "ok", "value": gpus * F * args.steps / el_g, "ms_per_step": el_g / args.steps * 1e3,
-                           "kernel_ms": km_g, "step_event_ms": stats_g})
+            measure_gather(wl, devs, args, dist, mode, rank, world, gpus, target)
             wd.cancel()
         except Exception as e:  # the line still reports the shards, with the gather's failure
             print("rank %d: gather failed: %r" % (rank, e), file=sys.stderr, flush=True)
-            gather["status"] = "failed on rank %d: %r" % (rank, e)
+            target["status"] = "failed on rank %d: %r" % (rank, e)
+            failed.append(target)
             if rank == 0:
                 emit_line()
-                os._exit(0)
+                os._exit(code)
             wd.t.join()  # a failed peer waits for its deadline (rank 0 may be blocked on it)
-    extras = {}
-    if mode == "one":
-        extras = secondary(args, plan, frames[d0], devs, n, F)
-    line_box.update(extras)
+    if c5 is not None and "gather" in c5 and c5["gather"].get("status") == "ok":
+        c5["gather"]["vs_shards"] = c5["gather"]["value"] / c5["value"]
     emit_line()
     if dist:
         dist.barrier()
@@ -484,35 +637,51 @@ def main():
 
 
 def secondary(args, plan, frames, devs, n, F):
-    """Single-GPU secondary fields (never `value`): fast precision, config C4 exactly, every
-    output, the live PMC counters, the PCIe-inclusive host path and the CPU baseline."""
+    """Single-GPU secondary fields (never `value`): fast precision, configs C3 and C4 exactly,
+    the reference-order MFCC, every output, the live PMC counters, the PCIe-inclusive host path,
+    the facade's real-time latency and the CPU baselines."""
     out = {}
     dev = devs.devs[0]
 
-    def timed(p, feats, bytes_per_frame):
-        sets = [p.alloc_outputs(F, feats) for _ in range(2)]
+    def timed(p, feats, bytes_per_frame, fr=frames):
+        Fx = fr.shape[0]
+        sets = [p.alloc_outputs(Fx, feats) for _ in range(2)]
 
         def st(k):
-            p.extract_device(frames.data_ptr(), F, sets[k & 1][1], devs.stream(dev, k).cuda_stream)
+            p.extract_device(fr.data_ptr(), Fx, sets[k & 1][1], devs.stream(dev, k).cuda_stream)
         settle(st, devs, args.settle_ms)
         el, km, stats = run_mode(st, devs, args.steps, args.warmup, None)
         alone = stats["launch_alone_mean_ms"]
-        return {"value": F * args.steps / el, "unit": "frames/s", "kernel_ms": alone, "period_ms": km,
+        return {"value": Fx * args.steps / el, "unit": "frames/s", "kernel_ms": alone, "period_ms": km,
                 "bytes_per_frame": bytes_per_frame,
-                "roofline_frac": F * bytes_per_frame / (alone * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "frac_pipelined": F * bytes_per_frame / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                "roofline_frac": Fx * bytes_per_frame / (alone * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "frac_pipelined": Fx * bytes_per_frame / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
     if not args.no_fast and args.precision != "fast":
         # BASELINE.md: the fp32-butterfly mode beside the faithful one (same features and frames)
         out["fast_mode"] = dict(timed(capi.Plan(buffer_size=n, precision="fast", device=dev), FEATURES,
                                       4 * n + 4 * OUT_FLOATS), precision="fast (f32 butterflies; not bit-faithful)")
+    if not args.no_mfcc_exact and args.precision != "fast":
+        # north_star's "all features within 1e-5" per element for the MFCC too: the reference-order
+        # mel sums, log and DCT (MGX_FLAG_MFCC_REFERENCE), same features and frames as `value`
+        ex = timed(capi.Plan(buffer_size=n, precision=args.precision, mfcc_reference=True, device=dev), FEATURES,
+                   4 * n + 4 * OUT_FLOATS)
+        out["mfcc_exact"] = dict(ex, flag="MGX_FLAG_MFCC_REFERENCE (mfcc.js:53-93 in the reference's own order)")
     if not args.no_c4:
         # BASELINE config C4 exactly: 40-band mel + 13 MFCC, nothing else (SURVEY §8(d): 4,148 B/frame)
         out["c4"] = dict(timed(capi.Plan(buffer_size=n, precision=args.precision, num_mel_bands=40, device=dev),
                                ["mfcc"], 4 * n + 4 * 13), features=["mfcc"], mel_bands=40, mfcc_coeffs=13)
     if not args.no_c3:
         # BASELINE config C3: spectral* + loudness + perceptual (SURVEY §8(d): 4,232 B/frame)
-        feats3 = [f for f in FEATURES if f not in ("rms", "energy", "zcr", "mfcc")]
-        out["c3"] = dict(timed(plan, feats3, 4 * n + 4 * (7 + 25 + 2)), features=feats3)
+        out["c3"] = dict(timed(plan, C3_FEATURES, 4 * n + 4 * (7 + 25 + 2)), features=C3_FEATURES)
+    if not args.no_c2:
+        # BASELINE config C2: 65,536 frames x N = 512, amplitudeSpectrum + spectralCentroid (3,076 B/frame)
+        with torch.cuda.device(dev):
+            f2 = torch.empty(65536, 512, dtype=torch.float32, device="cuda:%d" % dev)
+            capi.synth_frames_device(f2, capi_seed())
+        out["c2"] = dict(timed(capi.Plan(buffer_size=512, precision=args.precision, device=dev),
+                               ["amplitudeSpectrum", "spectralCentroid"], 4 * 512 + 4 * 257, fr=f2),
+                         features=["amplitudeSpectrum", "spectralCentroid"], buffer_size=512, frames=65536)
+        del f2
     if not args.no_every_output:
         # EVERY output of the path -- the headline set plus the amplitude, power and complex
         # spectra -- with the 40-band mel of config C4, same frames
@@ -527,8 +696,19 @@ def secondary(args, plan, frames, devs, n, F):
             out["pmc"] = (None, None, "rocprofv3 passes failed: %r" % (e,))
     if not args.no_host_path:
         out["host_path"] = host_path(plan, frames)
+    if not args.no_latency:
+        try:
+            out["latency"] = latency_js()
+        except Exception as e:
+            out["latency"] = {"status": "failed: %r" % (e,)}
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+        cb = cpu_baseline(n, args.cpu_seconds)
+        out["cpu_baseline"] = cb
+        for key, c in cb.get("configs", {}).items():
+            if key in out and isinstance(out[key], dict):
+                out[key]["cpu_baseline"] = c
+        if "latency" in out and "c1" in cb.get("configs", {}):
+            out["latency"]["cpu_c1_us_per_call"] = cb["configs"]["c1"].get("value")
     return out
 
 
@@ -561,6 +741,12 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
         mf["tflops"] = mf["flop_per_launch"] / (km_s * 1e-3) / 1e12
         mf["peak_tflops"] = 78.6
         mf["frac"] = mf["tflops"] / mf["peak_tflops"]
+        c4 = valu.get("mfma_f64_c4")
+        c4_ms = (extras.get("c4") or {}).get("kernel_ms")
+        if c4 and c4_ms:
+            c4["tflops"] = c4["flop_per_launch"] / (c4_ms * 1e-3) / 1e12
+            c4["peak_tflops"] = 78.6
+            c4["frac"] = c4["tflops"] / c4["peak_tflops"]
     line = {
         "metric": "audio frames/sec (bufferSize=1024, all features) at 1/2/4/8 GPUs; % HBM roofline",
         "value": value,
@@ -604,9 +790,12 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
         line["gather"] = gather if gather is not None else {"status": "off (--no-gather or shared GPUs)"}
     if valu:
         line["valu"] = valu
-    for k in ("fast_mode", "c3", "c4", "every_output", "host_path", "cpu_baseline"):
+    for k in ("c5", "fast_mode", "mfcc_exact", "c2", "c3", "c4", "every_output", "host_path", "latency",
+              "cpu_baseline"):
         if k in extras:
             line[k] = extras[k]
+    if "mfcc_exact" in line and line["mfcc_exact"].get("kernel_ms"):
+        line["mfcc_exact"]["cost_vs_value_kernel"] = line["mfcc_exact"]["kernel_ms"] / kernel_ms - 1.0
     return line
 
 

@@ -160,7 +160,12 @@ int mgx_plan_destroy(mgx_plan* plan);
 int mgx_plan_get_desc(const mgx_plan* plan, mgx_plan_desc* out_desc);
 
 /* Device-resident batch: frames and every non-NULL output are device pointers.
- * Asynchronous on `stream` (hipStream_t or NULL). */
+ * Asynchronous on `stream` (hipStream_t or NULL). A plan with MGX_FLAG_MFCC_REFERENCE
+ * (and an MFCC output) also needs per-stream scratch: the power-row ring of its mel chains,
+ * one per distinct stream the plan launches on (~2 KB x 8 per resident wave, tens of MB),
+ * allocated on the first call on that stream (hipMalloc, which may synchronise the device:
+ * make one untimed call per stream first, outside any stream capture) and kept until
+ * mgx_plan_destroy. Plans without that flag allocate nothing here. */
 int mgx_extract_device(mgx_plan* plan, const float* frames, uint64_t num_frames,
                        const mgx_outputs* outputs, void* stream);
 
@@ -282,7 +287,9 @@ int mgx_group_destroy(mgx_group* group);
 int mgx_group_info(const mgx_group* group, uint32_t* nranks, uint32_t* first_local, uint32_t* num_local);
 /* What the RCCL communicator of this process's first local rank reports: ranks in the
  * communicator (ncclCommCount), this rank in it (ncclCommUserRank) and its device
- * (ncclCommCuDevice); all -1 when the group has no communicator (one rank, or device copies). */
+ * (ncclCommCuDevice); all -1 when the group has no communicator (one rank, or device copies).
+ * MGX_E_UNSUPPORTED when the loaded RCCL lacks those three queries (the data path does not
+ * need them). */
 int mgx_group_comm_info(const mgx_group* group, int32_t* comm_ranks, int32_t* comm_rank, int32_t* comm_device);
 
 /* Device-resident batch. frames[i]: device pointer of the shard of local rank

@@ -73,10 +73,12 @@ Rccl* rccl() {
   sym(r.Send, "ncclSend");
   sym(r.Recv, "ncclRecv");
   sym(r.GetErrorString, "ncclGetErrorString");
-  sym(r.CommCount, "ncclCommCount");
-  sym(r.CommUserRank, "ncclCommUserRank");
-  sym(r.CommCuDevice, "ncclCommCuDevice");
   r.ok = all;
+  // optional: they only feed the diagnostic mgx_group_comm_info, never the data path
+  auto opt = [&](auto& fn, const char* name) { fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name)); };
+  opt(r.CommCount, "ncclCommCount");
+  opt(r.CommUserRank, "ncclCommUserRank");
+  opt(r.CommCuDevice, "ncclCommCuDevice");
   return r.ok ? &r : nullptr;
 }
 
@@ -413,6 +415,8 @@ int mgx_group_comm_info(const mgx_group* g, int32_t* comm_ranks, int32_t* comm_r
     Rccl* r = rccl();
     int v;
     if (!r) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
+    if (!r->CommCount || !r->CommUserRank || !r->CommCuDevice)
+      return fail(MGX_E_UNSUPPORTED, "this RCCL lacks ncclCommCount / ncclCommUserRank / ncclCommCuDevice");
     if (r->CommCount(c, &v) != ncclSuccess) return fail(MGX_E_DEVICE, "ncclCommCount failed");
     n = v;
     if (r->CommUserRank(c, &v) != ncclSuccess) return fail(MGX_E_DEVICE, "ncclCommUserRank failed");

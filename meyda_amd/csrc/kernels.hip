@@ -902,8 +902,13 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
   if (lane < nf) rec.lm[lane] = mine[0].x + mine[1].y;  // nf <= kMaxMel = 64
 }
 
-// Bark-band sums and mel energies of a frame with a non-finite amplitude, summed exactly
-// as the reference does (see frame_phase1). The amplitude row is rewritten to the slot buffer.
+// float32 bits of 2^64: an amplitude a >= 2^64 has a * a = +inf in float32 (a < 2^64 stays
+// below FLT_MAX after rounding), i.e. an infinite power spectrum bin (powerSpectrum.js).
+constexpr uint32_t kPowOverflowBits = 0x5F800000u;
+
+// Bark-band sums and mel energies of a frame with a non-finite amplitude or power (or an
+// amplitude total of 2^64 or more), summed exactly as the reference does (see frame_phase1).
+// The amplitude row is rewritten to the slot buffer.
 template <int N>
 __device__ __forceinline__ void nonfinite_frame_sums(KArgs* ap, const float (&av)[Geo<N>::R], int lane,
                                                                float2* buf, FrameRec& rec, int lmo = 0) {
@@ -1320,7 +1325,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     uint32_t am = 0u;
 #pragma unroll
     for (int jj = 0; jj < R; ++jj) am = max(am, __builtin_bit_cast(uint32_t, av[jj]));
-    light_nonfinite = __ballot(am >= 0x7F800000u) != 0;
+    light_nonfinite = __ballot(am >= kPowOverflowBits) != 0;
   }
   MGX_MARK(moments_done);
   prio_hi<8>();
@@ -1432,9 +1437,13 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // zero weights turn Inf into NaN in every band). Such frames — wave-uniform, rare — take
   // the reference's own summation: bark bands bin by bin in double (loudness.js:47-66),
   // mel bands over all bins in reference order (mfcc.js:53-62).
-  // (total = sum of the amplitudes in double: non-finite iff some amplitude is.)
+  // (total = sum of the amplitudes in double: non-finite iff some amplitude is.) A finite
+  // amplitude of 2^64 or more has an infinite float32 power (powerSpectrum.js), which the
+  // reference's zero weights turn into NaN in every mel band (0 x Inf): such frames take the
+  // same path (a total of 2^64 or more is the cheap, conservative test: the path is the
+  // reference's own summation, right for any frame).
   MGX_MARK(bands_done);
-  const bool nonfinite = light ? light_nonfinite : !(total < __builtin_huge_val());
+  const bool nonfinite = light ? light_nonfinite : !(total < 0x1p64);
   if (nonfinite) {
     // (CHAIN with paired batches: the pair's first batch keeps its mel sums in the upper half of lm)
     nonfinite_frame_sums<N>(ap, av, lane, buf, rec, CHAIN && ap->chain_pair && !(it & 1) ? 32 : 0);

@@ -416,8 +416,15 @@ struct mgx_plan {
   int chain_groups = 0;  // MGX_FLAG_MFCC_REFERENCE: 8-step groups of the mel chains (chain_schedule)
   int chain_pair = 0;  // ... over two consecutive batches of a wave (8 frames)
   // the mel chains' power-row rings (kernels.hip KGeo::GROWS), one per stream a launch used: the
-  // launches of one stream run in order, those of two streams may overlap
-  std::vector<std::pair<void*, float*>> chain_rings;
+  // launches of one stream run in order, those of two streams may overlap. Each ring's event is
+  // recorded after every launch that uses it, so destroy waits for exactly those launches (the
+  // stream itself may be gone by then).
+  struct ChainRing {
+    void* stream;
+    float* rows;
+    hipEvent_t done;
+  };
+  std::vector<ChainRing> chain_rings;
   // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
   float* s_frames[2] = {nullptr, nullptr};
   unsigned char* s_out[2] = {nullptr, nullptr};
@@ -611,8 +618,11 @@ int mgx_plan_destroy(mgx_plan* p) {
   if (!p) return MGX_OK;
   (void)hipSetDevice(p->d.device);
   if (p->dev) (void)hipFree(p->dev);
-  if (!p->chain_rings.empty()) (void)hipDeviceSynchronize();
-  for (auto& r : p->chain_rings) (void)hipFree(r.second);
+  for (auto& r : p->chain_rings) {
+    (void)hipEventSynchronize(r.done);
+    (void)hipEventDestroy(r.done);
+    (void)hipFree(r.rows);
+  }
   if (p->s_copy) (void)hipStreamSynchronize(p->s_copy);
   if (p->s_comp) (void)hipStreamSynchronize(p->s_comp);
   for (int i = 0; i < 2; ++i) {
@@ -677,19 +687,33 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.wg_ranks = grid == p->grid_cap && p->cus > 0 ? p->grid_cap / p->cus : 1;
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  hipEvent_t ring_done = nullptr;
   if (a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) {
     for (auto& r : p->chain_rings)
-      if (r.first == stream) a.chain_rows = r.second;
+      if (r.stream == stream) {
+        a.chain_rows = r.rows;
+        ring_done = r.done;
+      }
     if (!a.chain_rows) {
-      // 2 FPW x N/2 floats for each wave of the largest grid (4 waves per workgroup)
+      // 2 FPW x N/2 floats for each wave of the largest grid (4 waves per workgroup); the first
+      // launch on a stream allocates its ring (include/meyda_gpu.h)
       const size_t bytes = (size_t)p->grid_cap * 4 * 2 * (size_t)(fb / 4) * (size_t)p->L * sizeof(float);
       e = hipMalloc(reinterpret_cast<void**>(&a.chain_rows), bytes);
       if (e != hipSuccess) return hip_fail(e, "hipMalloc(mel chain rows)");
-      p->chain_rings.emplace_back(stream, a.chain_rows);
+      e = hipEventCreateWithFlags(&ring_done, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        (void)hipFree(a.chain_rows);
+        return hip_fail(e, "hipEventCreate(mel chain rows)");
+      }
+      p->chain_rings.push_back({stream, a.chain_rows, ring_done});
     }
   }
   e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "extract kernel launch");
+  if (ring_done) {
+    e = hipEventRecord(ring_done, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord(mel chain rows)");
+  }
   return MGX_OK;
 }
 

@@ -232,11 +232,19 @@ class CpuMeyda {
   }
 
   // Every feature of one frame x (Float32Array(n)): sc = Float64Array(13) in the record
-  // order of include/meyda_gpu.h, spec = Float32Array(24), mf = Float32Array(13).
-  frame(x, sc, spec, mf) {
+  // order of include/meyda_gpu.h, spec = Float32Array(24), mf = Float32Array(13) (null: no
+  // MFCC); noTime skips rms, energy and zcr (config C3's feature set).
+  frame(x, sc, spec, mf, noTime) {
     const { n, L, sr } = this;
     const a = this.spectrum(x);
-    // a12-a14 on the unwindowed signal
+    if (!noTime) this.timeFeatures(x, sc);
+    this.spectralFeatures(a, sc, spec);
+    if (mf) this.mfcc(mf);
+  }
+
+  // a12-a14 on the unwindowed signal
+  timeFeatures(x, sc) {
+    const n = this.n;
     let e = 0;
     for (let i = 0; i < n; i++) e += x[i] * x[i];
     let z = 0;
@@ -246,6 +254,11 @@ class CpuMeyda {
     sc[0] = Math.sqrt(e / n);
     sc[1] = e;
     sc[2] = z;
+  }
+
+  // a18-a28 of the amplitude spectrum a (this.amp)
+  spectralFeatures(a, sc, spec) {
+    const { n, L, sr } = this;
     // a18, a22-a24: mu per feature (the reference calls mu inside each extractor)
     const ref = this.layout !== 'batch';
     const m1 = mu(1, a);
@@ -298,7 +311,6 @@ class CpuMeyda {
     let sh = 0;
     for (let i = 0; i < NUM_BARK; i++) sh += i < 15 ? (i + 1) * loud.specific[i + 1] : 0.066 * Math.exp(0.171 * (i + 1));
     sc[12] = sh * (0.11 / loud.total);
-    if (mf) this.mfcc(mf);
   }
 
   // F frames (Float32Array(F * n)) -> structure of arrays (scalars F x 13, specific F x 24,

@@ -160,3 +160,29 @@ def test_bench_value_is_the_shards_rate():
     failed = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, st,
                               {"status": "failed on rank 3"}, {})
     assert failed["value"] == 3.5e9 and failed["config"]["gather_to_rank0"] is False
+
+
+def test_bench_c5_field_shape():
+    """Config C5 (BASELINE.json configs[4]: N = 2048, all features incl. MFCC, 262,144 frames per
+    GPU, RCCL gather) is a field of every line: at N = 1 its gather is reported as skipped, at
+    N > 1 it starts as "not run" and, once measured, carries the gather-inclusive rate beside
+    the shards' (vs_shards), never replacing `value`."""
+    import types
+
+    import bench
+    st = {"launch_alone_mean_ms": 1.3}
+    one = bench.c5_field(1, 262144, 0.026, 1.3, st, 20, False)
+    assert one["buffer_size"] == 2048 and one["frames_per_gpu"] == 262144 and one["frames_total"] == 262144
+    assert one["bytes_per_frame"] == 4 * 2048 + 4 * 50 and one["features"] == bench.FEATURES
+    assert one["gather"]["status"].startswith("skipped (1 GPU)")
+    assert abs(one["value"] - 262144 * 20 / 0.026) < 1e-6 * one["value"]
+    assert abs(one["roofline_frac"] - 262144 * 8392 / 1.3e-3 / 8e12) < 1e-12
+    eight = bench.c5_field(8, 262144, 0.027, 1.35, {"rank0": st, "per_rank_period_ms": [1.35] * 8}, 20, True)
+    assert eight["frames_total"] == 2097152 and eight["gather"]["status"] == "not run"
+    assert eight["kernel_ms"] == 1.3
+    args = types.SimpleNamespace(steps=20, warmup=5, precision="faithful", single_stream=False)
+    line = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, {"launch_alone_mean_ms": 0.6},
+                            {"status": "ok", "value": 2.8e9}, {"c5": eight})
+    assert line["value"] == 3.5e9 and line["c5"]["frames_total"] == 2097152
+    p = bench.parse([])
+    assert not p.no_c5 and p.c5_frames == 262144 and not p.strict_gather

@@ -77,15 +77,19 @@ def test_group_argument_errors(capi):
         g.extract_device([0], [0], capi.Outputs(), capi.OUT_MFCC)
 
 
-def test_multi_device_gather(capi):
-    """Two or more devices in one process: shards, chunked RCCL gather to device 0."""
+@pytest.mark.parametrize("n,F", [(1024, 40000), (2048, 40003)])
+def test_multi_device_gather(capi, n, F):
+    """Every visible device in one process: ragged shards, 8-chunk RCCL gather to device 0 of
+    every output bench.py gathers (13 scalars + loudness.specific + MFCC; at N = 2048 config
+    C5's), byte-identical to one plan's extraction of the whole batch."""
     import torch
     ndev = capi.device_count()
     if ndev < 2:
         pytest.skip("one device visible: the RCCL gather needs two (covered on the multi-GPU node)")
-    devs = list(range(min(ndev, 4)))
-    n, F = 1024, 40000
+    devs = list(range(ndev))
     g = capi.Group(buffer_size=n, devices=devs, scalar_f64=True)
+    assert (g.nranks, g.first_local, g.num_local) == (len(devs), 0, len(devs))
+    assert g.comm_info() == (len(devs), 0, 0)
     counts = [capi.shard_range(F, len(devs), r)[1] for r in range(len(devs))]
     starts = [capi.shard_range(F, len(devs), r)[0] for r in range(len(devs))]
     xs = []
@@ -93,17 +97,21 @@ def test_multi_device_gather(capi):
         with torch.cuda.device(d):
             xs.append(_frames(capi, c, n, first=s))
     plan = capi.Plan(buffer_size=n, scalar_f64=True)
-    feats = ["rms", "spectralKurtosis", "loudness", "mfcc", "amplitudeSpectrum"]
+    feats = capi.ALL_FEATURES
     got, o = plan.alloc_outputs(F, feats)
+    for v in got.values():
+        v.fill_(float("nan"))
     for dd in devs:
         torch.cuda.synchronize(dd)
-    g.extract_device([t.data_ptr() for t in xs], counts, o, capi.output_mask(o), num_chunks=4)
+    g.extract_device([t.data_ptr() for t in xs], counts, o, capi.output_mask(o), num_chunks=8)
     for dd in devs:
         torch.cuda.synchronize(dd)
     want = plan.extract_torch(_frames(capi, F, n), feats)
     torch.cuda.synchronize()
     for k in want:
-        assert torch.equal(got[k], want[k]), k
+        assert torch.equal(got[k].view(torch.int64) if got[k].dtype == torch.float64 else got[k].view(torch.int32),
+                           want[k].view(torch.int64) if want[k].dtype == torch.float64 else want[k].view(torch.int32)), k
+    g.close()
 
 
 @pytest.mark.parametrize("ranks,nch", [(2, 1), (3, 8), (4, 3)])

@@ -153,3 +153,29 @@ def test_chain_overflowing_band_then_next_chain(capi, oracle_mod):
     g = out["mfcc"]
     assert not np.isnan(g).any(), g[:, :4]
     assert np.array_equal(g, r), (g[:, :4], r[:, :4])
+
+
+@pytest.mark.parametrize("reference", [False, True])
+@pytest.mark.parametrize("n", [512, 1024, 2048])
+def test_finite_amplitude_infinite_power(capi, oracle_mod, n, reference):
+    """A loud tone whose amplitude bins stay finite but whose float32 power overflows (|X| above
+    2^64, powerSpectrum.js a * a = +inf): the reference multiplies every bin by every band's weight
+    (mfcc.js:56-61), so 0 x inf makes every band, and every coefficient, NaN. Both MFCC paths must
+    send such a frame to the reference's own bin-by-bin sums, whatever the other features do."""
+    t = np.arange(n, dtype=np.float64)
+    x = []
+    for a, k in ((1.2e20 / np.sqrt(n), n // 10), (2.0e20 / np.sqrt(n), n // 3)):  # peak |X| ~ a sqrt(n) / 4
+        x.append((a * np.sin(2 * np.pi * k * t / n + 0.3) + np.random.default_rng(k).uniform(-1, 1, n)).astype(np.float32))
+    x.append(np.random.default_rng(3).uniform(-1, 1, n).astype(np.float32))  # an ordinary frame beside them
+    x = np.stack(x)
+    ref = oracle_mod.extract(x)
+    assert np.isfinite(ref["amp"][:2]).all() and (ref["amp"][:2].max(1) >= 2.0 ** 64).all()
+    assert np.isnan(ref["mfcc"][:2]).all()
+    plan = capi.Plan(buffer_size=n, scalar_f64=True, mfcc_reference=reference)
+    out = plan.extract(x, FEATS)
+    assert np.isnan(out["mfcc"][:2]).all(), out["mfcc"][:2, :4]
+    assert not tolerance.check_vectors(out["mfcc"][2:], ref["mfcc"][2:])
+    for feats in (["mfcc"], ["mfcc", "spectralCentroid"]):  # the light and the subset kernels
+        sub = plan.extract(x, feats)
+        assert np.isnan(sub["mfcc"][:2]).all(), (feats, sub["mfcc"][:2, :4])
+    compare(out, ref, n)

@@ -15,7 +15,8 @@ prec = os.environ.get("PROBE_PREC", "faithful")
 F = 262144
 frames = torch.empty(F, n, dtype=torch.float32, device="cuda")
 capi.synth_frames_device(frames, 0x6D657964)
-plan = capi.Plan(buffer_size=n, precision=prec, dct_sequential=bool(int(os.environ.get("MGX_PROBE_FLAGS", "0")) & 1))
+plan = capi.Plan(buffer_size=n, precision=prec, num_mel_bands=int(os.environ.get("PROBE_BANDS", "26")),
+                 dct_sequential=bool(int(os.environ.get("MGX_PROBE_FLAGS", "0")) & 1))
 _, o = plan.alloc_outputs(F, feats)
 for _ in range(int(os.environ.get("PROBE_REPS", "3"))):
     plan.extract_device(frames.data_ptr(), F, o, torch.cuda.current_stream().cuda_stream)
