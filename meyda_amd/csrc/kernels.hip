@@ -1079,13 +1079,17 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       plt = l;
     }
   } else {
+    // without NaN samples x >= 0 is the complement of x < 0, so a sign change between samples
+    // i and i + 1 is bit i of s ^ (s >> 1) over the frame's sign sequence s (sample 64 c + l is
+    // bit l of chunk c's ballot): the chunk's 63 inner pairs and, in bit 63, the pair it forms
+    // with the next chunk's first sample (the last chunk's bit 63 compares with itself: 0)
+    uint64_t l[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) l[c] = __ballot(x[c] < 0.0f);
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      const uint64_t l = __ballot(x[c] < 0.0f), g = ~l;
-      z += __popcll(((g & (l >> 1)) | (l & (g >> 1))) & 0x7FFFFFFFFFFFFFFFull);
-      if (c > 0) z += (int)((((pge >> 63) & l) | ((plt >> 63) & g)) & 1ull);
-      pge = g;
-      plt = l;
+      const uint64_t nxt = c + 1 < CH ? l[c + 1] << 63 : l[c] & 0x8000000000000000ull;
+      z += __popcll(l[c] ^ ((l[c] >> 1) | nxt));
     }
   }
   // float32 partial sums are within 1e-6 relative of the double sum; a wave whose

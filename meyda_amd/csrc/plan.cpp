@@ -44,6 +44,12 @@ using mgx::fail;
 using mgx::hip_fail;
 
 const uint64_t kHostChunk = 65536;              // frames per host-staging chunk
+// Host batches of at most this many frames (a real-time buffer, or a streaming batch of K
+// buffers) skip the device staging: the frames are copied into plan-owned pinned host memory
+// that the kernel reads over PCIe itself, and it writes the features back there (no DMA copies,
+// no cross-stream events: one launch and one stream synchronisation per call). Overridden by
+// $MGX_SMALL_BATCH_FRAMES at plan creation (0: always the staged path).
+const uint64_t kSmallBatchFrames = 512;
 const double kJsPi = 3.141592653589793;        // Math.PI
 const double kJsSqrt1_2 = 0.7071067811865476;  // Math.SQRT1_2
 
@@ -434,6 +440,11 @@ struct mgx_plan {
   uint64_t s_pcm_bytes = 0;
   hipStream_t s_copy = nullptr, s_comp = nullptr;
   hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr}, ev_back[2] = {nullptr, nullptr};
+  // small host batches (kSmallBatchFrames): pinned, device-mapped, coherent host buffers
+  uint64_t small_max = kSmallBatchFrames;
+  float* h_in = nullptr;
+  unsigned char* h_out = nullptr;
+  size_t h_in_bytes = 0, h_out_bytes = 0;
 };
 
 extern "C" {
@@ -573,6 +584,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
     if (strcmp(gc, "print") == 0) fprintf(stderr, "mgx: grid_cap %d (%d CUs)\n", p->grid_cap, prop.multiProcessorCount);
     else if (atoi(gc) > 0) p->grid_cap = atoi(gc);
   }
+  if (const char* sb = getenv("MGX_SMALL_BATCH_FRAMES")) p->small_max = (uint64_t)std::max(0, atoi(sb));
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
@@ -634,6 +646,8 @@ int mgx_plan_destroy(mgx_plan* p) {
   }
   if (p->s_copy) (void)hipStreamDestroy(p->s_copy);
   if (p->s_comp) (void)hipStreamDestroy(p->s_comp);
+  if (p->h_in) (void)hipHostFree(p->h_in);
+  if (p->h_out) (void)hipHostFree(p->h_out);
   delete p;
   return MGX_OK;
 }
@@ -759,6 +773,107 @@ int ensure_host_staging(mgx_plan* p, uint64_t chunk, size_t out_bytes) {
   return MGX_OK;
 }
 
+// Device bytes per frame of the requested outputs (host staging layouts).
+size_t out_bytes_per_frame(const mgx_plan* p, const mgx_outputs* o) {
+  const size_t ss = p->d.scalar_f64 ? 8 : 4;
+  size_t per = 0;
+  for (int i = 0; i < MGX_NUM_SCALARS; ++i) per += o->scalars[i] ? ss : 0;
+  per += (o->loudness_specific ? (size_t)mgx::kBark * 4 : 0) + (o->mfcc ? (size_t)p->d.num_mfcc_coeffs * 4 : 0) +
+         (o->amplitude_spectrum ? (size_t)p->L * 4 : 0) + (o->power_spectrum ? (size_t)p->L * 4 : 0) +
+         (o->complex_real ? 2 * (size_t)p->n * 4 : 0);
+  return per;
+}
+
+// A small host batch (at most p->small_max frames): the frames into the plan's pinned input
+// buffer, one launch that reads them over PCIe and writes the features into the pinned output
+// buffer, one synchronisation, the features out to the caller's arrays. `fill(dst)` writes the
+// batch's float32 frames to host memory at dst. The buffers are coherent (fine-grained) host
+// memory mapped into the device, so no cache of either side holds a stale copy between calls.
+template <typename Fill>
+int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill fill) {
+  const int n = p->n, L = p->L;
+  const size_t ss = p->d.scalar_f64 ? 8 : 4;
+  const size_t nb = mgx::kBark, nc = p->d.num_mfcc_coeffs;
+  const size_t in_bytes = nframes * (size_t)n * sizeof(float);
+  const size_t out_bytes = out_bytes_per_frame(p, o) * nframes + 20 * 256;
+  hipError_t e = hipSetDevice(p->d.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if (!p->s_comp) {
+    e = hipStreamCreateWithFlags(&p->s_comp, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+  }
+  if (p->h_in_bytes < in_bytes) {
+    if (p->h_in) (void)hipHostFree(p->h_in);
+    p->h_in = nullptr;
+    p->h_in_bytes = 0;
+    const size_t want = std::max<size_t>(in_bytes, 16 * (size_t)n * sizeof(float));
+    e = hipHostMalloc(reinterpret_cast<void**>(&p->h_in), want, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(small batch frames)");
+    p->h_in_bytes = want;
+  }
+  if (p->h_out_bytes < out_bytes) {
+    if (p->h_out) (void)hipHostFree(p->h_out);
+    p->h_out = nullptr;
+    p->h_out_bytes = 0;
+    e = hipHostMalloc(reinterpret_cast<void**>(&p->h_out), out_bytes, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(small batch outputs)");
+    p->h_out_bytes = out_bytes;
+  }
+  int rc = fill(p->h_in);
+  if (rc) return rc;
+  void* din = nullptr;
+  void* dout = nullptr;
+  e = hipHostGetDevicePointer(&din, p->h_in, 0);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(&dout, p->h_out, 0);
+  if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
+  mgx_outputs d{};
+  const mgx_outputs h = [&] {  // the same layout, host addresses
+    mgx_outputs r{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t at = off; off += (bytes + 255) / 256 * 256; return at; };
+    size_t at[19];
+    for (int k = 0; k < MGX_NUM_SCALARS; ++k) at[k] = o->scalars[k] ? take(nframes * ss) : 0;
+    at[13] = o->loudness_specific ? take(nframes * nb * 4) : 0;
+    at[14] = o->mfcc ? take(nframes * nc * 4) : 0;
+    at[15] = o->amplitude_spectrum ? take(nframes * L * 4) : 0;
+    at[16] = o->power_spectrum ? take(nframes * L * 4) : 0;
+    at[17] = o->complex_real ? take(nframes * (size_t)n * 4) : 0;
+    at[18] = o->complex_imag ? take(nframes * (size_t)n * 4) : 0;
+    unsigned char* dv = static_cast<unsigned char*>(dout);
+    for (int k = 0; k < MGX_NUM_SCALARS; ++k) {
+      d.scalars[k] = o->scalars[k] ? dv + at[k] : nullptr;
+      r.scalars[k] = o->scalars[k] ? p->h_out + at[k] : nullptr;
+    }
+    auto both = [&](bool want, size_t a, float*& dd, float*& hh) {
+      dd = want ? reinterpret_cast<float*>(dv + a) : nullptr;
+      hh = want ? reinterpret_cast<float*>(p->h_out + a) : nullptr;
+    };
+    both(o->loudness_specific, at[13], d.loudness_specific, r.loudness_specific);
+    both(o->mfcc, at[14], d.mfcc, r.mfcc);
+    both(o->amplitude_spectrum, at[15], d.amplitude_spectrum, r.amplitude_spectrum);
+    both(o->power_spectrum, at[16], d.power_spectrum, r.power_spectrum);
+    both(o->complex_real, at[17], d.complex_real, r.complex_real);
+    both(o->complex_imag, at[18], d.complex_imag, r.complex_imag);
+    return r;
+  }();
+  rc = mgx_extract_device(p, static_cast<const float*>(din), nframes, &d, p->s_comp);
+  if (rc) {
+    (void)hipStreamSynchronize(p->s_comp);
+    return rc;
+  }
+  e = hipStreamSynchronize(p->s_comp);
+  if (e != hipSuccess) return hip_fail(e, "small host batch");
+  for (int k = 0; k < MGX_NUM_SCALARS; ++k)
+    if (o->scalars[k]) memcpy(o->scalars[k], h.scalars[k], nframes * ss);
+  if (o->loudness_specific) memcpy(o->loudness_specific, h.loudness_specific, nframes * nb * 4);
+  if (o->mfcc) memcpy(o->mfcc, h.mfcc, nframes * nc * 4);
+  if (o->amplitude_spectrum) memcpy(o->amplitude_spectrum, h.amplitude_spectrum, nframes * L * 4);
+  if (o->power_spectrum) memcpy(o->power_spectrum, h.power_spectrum, nframes * L * 4);
+  if (o->complex_real) memcpy(o->complex_real, h.complex_real, nframes * (size_t)n * 4);
+  if (o->complex_imag) memcpy(o->complex_imag, h.complex_imag, nframes * (size_t)n * 4);
+  return MGX_OK;
+}
+
 template <typename Fill>
 int extract_host_chunked(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill fill) {
   const int n = p->n, L = p->L;
@@ -856,6 +971,11 @@ int mgx_extract_host(mgx_plan* p, const float* frames, uint64_t nframes, const m
   if ((o->complex_real == nullptr) != (o->complex_imag == nullptr))
     return fail(MGX_E_INVALID_ARGUMENT, "complex_real and complex_imag must be given together");
   const int n = p->n;
+  if (nframes <= p->small_max)
+    return extract_host_small(p, nframes, o, [&](float* dst) {
+      memcpy(dst, frames, nframes * (size_t)n * sizeof(float));
+      return MGX_OK;
+    });
   return extract_host_chunked(p, nframes, o, [&](uint64_t f0, uint64_t cnt, int slot, hipStream_t st) {
     hipError_t e = hipMemcpyAsync(p->s_frames[slot], frames + f0 * n, cnt * n * sizeof(float), hipMemcpyHostToDevice, st);
     return e == hipSuccess ? MGX_OK : hip_fail(e, "hipMemcpyAsync(frames)");

@@ -277,3 +277,37 @@ def test_errors_and_empty(capi):
     assert capi.lib().mgx_extract_host(plan._h, x.ctypes.data, 1, ctypes.byref(o)) == -1
     with pytest.raises(capi.MgxError):
         capi.Plan(buffer_size=128)  # below the GPU path's range: MGX_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("n", [512, 1024, 2048])
+def test_small_host_batches_equal_staged_path(capi, n):
+    """Host batches of up to 512 frames (the real-time get()/process() path) run one launch over
+    plan-owned pinned host memory that the kernel reads and writes over PCIe (plan.cpp
+    extract_host_small); larger ones stage through device memory. Both must give the device
+    path's outputs bit for bit: 1 frame, a streaming batch, the threshold and one past it, with
+    every output (the complex spectrum too) and with a two-feature request."""
+    import os
+
+    import torch
+    rng = np.random.default_rng(n)
+    os.environ["MGX_SMALL_BATCH_FRAMES"] = "0"
+    try:
+        staged = capi.Plan(buffer_size=n, scalar_f64=True)
+    finally:
+        del os.environ["MGX_SMALL_BATCH_FRAMES"]
+    small = capi.Plan(buffer_size=n, scalar_f64=True)
+    every = capi.ALL_FEATURES + ["amplitudeSpectrum", "powerSpectrum", "complexSpectrum"]
+    for F, feats in ((1, ["rms", "spectralCentroid"]), (1, every), (64, every), (512, every), (513, every)):
+        x = rng.uniform(-1, 1, (F, n)).astype(np.float32)
+        x[0, :7] = [np.nan, np.inf, -0.0, 1e-40, 3e38, -3e38, 0.0] if F > 1 else x[0, :7]
+        a, b = small.extract(x, feats), staged.extract(x, feats)
+        d = small.extract_torch(torch.from_numpy(x).cuda(), feats)
+        torch.cuda.synchronize()
+        for k in a:
+            assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), (F, k)
+            assert np.array_equal(a[k].view(np.uint8), d[k].cpu().numpy().view(np.uint8)), (F, k)
+        # the pinned buffers are reused: a second call with other frames must not see the first's
+        y = rng.uniform(-1, 1, (F, n)).astype(np.float32)
+        a2, b2 = small.extract(y, feats), staged.extract(y, feats)
+        for k in a2:
+            assert np.array_equal(a2[k].view(np.uint8), b2[k].view(np.uint8)), (F, k, "second call")
