@@ -186,3 +186,29 @@ def test_bench_c5_field_shape():
     assert line["value"] == 3.5e9 and line["c5"]["frames_total"] == 2097152
     p = bench.parse([])
     assert not p.no_c5 and p.c5_frames == 262144 and not p.strict_gather
+
+
+def test_bench_line_carries_every_config():
+    """The N = 1 line carries every BASELINE config beside `value` (C2, C3, C4, C5), the
+    reference-order MFCC's rate with its cost against the headline kernel, the real-time latency
+    and the C4 MFMA counters priced at C4's own launch time; none of them replaces `value`."""
+    import types
+
+    import bench
+    args = types.SimpleNamespace(steps=20, warmup=5, precision="faithful", single_stream=False)
+    st = {"launch_alone_mean_ms": 0.6}
+    mf = {"instr_per_launch": 655360.0, "flop_per_launch": 512 * 655360.0, "busy_cycles_per_launch": 1.0,
+          "gui_active_cycles": 1.0}
+    valu = {"instr_per_frame": 1200.0, "cvt_per_frame": 400.0, "f64_per_frame": 450.0, "lds_per_frame": 97.0,
+            "mfma_f64": dict(mf, flop_per_launch=512 * 458752.0), "mfma_f64_c4": dict(mf)}
+    extras = {"pmc": (1.13e9, valu, "note"), "c2": {"value": 1e9}, "c3": {"value": 5e8}, "c4": {"value": 5e8, "kernel_ms": 0.5},
+              "c5": bench.c5_field(1, 262144, 0.026, 1.3, {"launch_alone_mean_ms": 1.3}, 20, False),
+              "mfcc_exact": {"value": 3.6e8, "kernel_ms": 0.75}, "latency": {"status": "ok", "c1": {"us_per_call": 25.0}}}
+    line = bench.build_line(args, 1, "one", [], 262144, 1024, 4.5e8, 0.0116, 0.58, st, None, extras)
+    assert line["value"] == 4.5e8 and "gather" not in line
+    for k in ("c2", "c3", "c4", "c5", "mfcc_exact", "latency"):
+        assert k in line, k
+    assert abs(line["mfcc_exact"]["cost_vs_value_kernel"] - 0.25) < 1e-12
+    c4 = line["valu"]["mfma_f64_c4"]
+    assert abs(c4["tflops"] - 512 * 655360.0 / 0.5e-3 / 1e12) < 1e-9 and c4["peak_tflops"] == 78.6
+    assert line["roofline"]["traffic"] == 1.13e9 and line["roofline"]["kernel_ms"] == 0.6

@@ -11,8 +11,9 @@ step() { echo "[refresh] $1"; }
 step tests
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
-step op_rates
-if [ -x tools/ubench/op_rates ]; then timeout -k 10 120 ./tools/ubench/op_rates > $O/op_rates.log 2>&1 || exit 1; fi
+step latency
+timeout -k 10 300 python tools/host_latency.py > $O/host_latency.log 2>&1 || { tail -20 $O/host_latency.log; exit 1; }
+timeout -k 10 300 node tools/latency.js >> $O/host_latency.log 2>&1 || { tail -20 $O/host_latency.log; exit 1; }
 step variants
 timeout -k 10 300 python tools/prof_variants.py ${VARIANT_NS:-256 512 1024 2048} > $O/variants.log 2>&1 || exit 1
 step configs
@@ -24,7 +25,7 @@ timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log
 tail -1 $O/bench.log
 step rocprof
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 100 --warmup 20 --single-stream --no-cpu-baseline --no-host-path --no-pmc --no-every-output --no-fast --no-c3 --no-c4 > $O/prof_bench.log 2>&1 || { tail -20 $O/prof_bench.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 100 --warmup 20 --single-stream --no-cpu-baseline --no-host-path --no-pmc --no-every-output --no-fast --no-c2 --no-c3 --no-c4 --no-c5 --no-mfcc-exact --no-latency > $O/prof_bench.log 2>&1 || { tail -20 $O/prof_bench.log; exit 1; }
 tail -1 $O/prof_bench.log
 # the 100 timed (pipelined) launches' period, then the 20 single-stream launches after them
 python3 $R/tools/prof_summary.py $O/prof/run_kernel_trace.csv 100 "" 1 20 > $O/prof_summary.txt

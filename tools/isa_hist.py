@@ -7,9 +7,8 @@ from collections import Counter
 
 
 def body(path, n=1024, faith=1, lit=0):
-    names = ["_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb%dELb%dELb0ELb0ELb0EEEvNS_10KernelArgsE" % (n, faith, lit),
-             "_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb%dELb%dELb0EEEvNS_10KernelArgsE" % (n, faith, lit),
-             "_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb%dELb%dEEEvNS_10KernelArgsE" % (n, faith, lit)]
+    names = ["_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb%dELb%dELb0ELb0ELb0ELb0EEEvNS_10KernelArgsE" % (n, faith, lit),
+             "_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb%dELb%dELb0ELb0ELb0EEEvNS_10KernelArgsE" % (n, faith, lit)]
     lines = open(path).read().split("\n")
     start = [i for i, l in enumerate(lines) if any(l.startswith(nm + ":") for nm in names)][0]
     out = []
