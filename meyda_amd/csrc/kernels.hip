@@ -92,8 +92,7 @@ struct Geo {
   // needs, against the 11.5 KB table it replaces; the workgroup keeps 5 per CU with the
   // LDS twiddles)
   static constexpr int SLOT_PHYS =
-      cmax(cmax(cmax(phys<N>(L - 1) + 1, L + 1), cmax(L + 2 * (L >> 5) + 1, 2 * (kMaxMel + 2 + 64) * 4 / 8)),
-           N == 512 ? 5 * 72 : 0);
+      cmax(cmax(cmax(phys<N>(L - 1) + 1, L + 1), cmax(L + 2 * (L >> 5) + 1, R * 64 + 2)), N == 512 ? 5 * 72 : 0);
   // Moment sums through an LDS transpose (5 rows of 64 doubles per wave, row stride 72 so
   // the rows read together fall in different banks) rather than 5 DPP wave sums: measured
   // faster at every N (at 2048 once it ran in the slot buffer: a table of its own cost 3 waves
@@ -779,7 +778,7 @@ struct Lds {
   // sums and the mel segment sums (mel_energies) in turn.
   static constexpr size_t slot_off = 0;
   static constexpr size_t slot_bytes = (size_t)4 * G::SLOT_PHYS * 8;
-  static_assert((size_t)G::SLOT_PHYS * 8 >= (size_t)2 * (kMaxMel + 2 + 64) * 4, "mel scratch must fit");
+  static_assert(G::SLOT_PHYS >= G::R * 64 + 2, "the dense mel entries (mel_energies) must fit the slot buffer");
   // Per wave, the 5 x 64 table of moment partials (transposed reduction) when it is not in
   // the slot buffer (MOM_SLOT: only N = 256 keeps a table of its own).
   static constexpr size_t mom_off = slot_off + slot_bytes;
@@ -836,12 +835,17 @@ struct MelTab {
 #pragma unroll
     for (int i = 0; i < W; ++i) w[i] = src[i];
   }
-  __device__ __forceinline__ float rise(int jj) const { return __builtin_bit_cast(float, w[jj]); }
-  __device__ __forceinline__ uint32_t slot(int jj) const { return (w[R + jj / 4] >> (8 * (jj % 4))) & 0xFFu; }
-  __device__ __forceinline__ float keep(int jj) const { return (float)((w[R + B + jj / 4] >> (8 * (jj % 4))) & 0xFFu); }
-  __device__ __forceinline__ float scan_keep(int s) const { return (float)((w[R + 2 * B + s / 4] >> (8 * (s % 4))) & 0xFFu); }
-  __device__ __forceinline__ uint32_t head_slot() const { return (w[R + 2 * B + 1] >> 16) & 0xFFu; }
-  __device__ __forceinline__ uint32_t tail_slot() const { return w[R + 2 * B + 1] >> 24; }
+  static constexpr int WW = mel_weight_words(R);
+  // (rise, fall) of bin jj: the stored pair, or the rising weight and 1 - rising in float32
+  __device__ __forceinline__ f32x2 weights(int jj) const {
+    if constexpr (WW == 2 * R) return f32x2{__builtin_bit_cast(float, w[2 * jj]), __builtin_bit_cast(float, w[2 * jj + 1])};
+    const float up = __builtin_bit_cast(float, w[jj]);
+    return f32x2{up, 1.0f - up};
+  }
+  __device__ __forceinline__ float keep(int jj) const { return (float)((w[WW + jj / 4] >> (8 * (jj % 4))) & 0xFFu); }
+  __device__ __forceinline__ float scan_keep(int s) const { return (float)((w[WW + B + s / 4] >> (8 * (s % 4))) & 0xFFu); }
+  __device__ __forceinline__ uint32_t asm_u() const { return w[WW + B + 2]; }  // byte offsets of U_band
+  __device__ __forceinline__ uint32_t asm_d() const { return w[WW + B + 3]; }  // ... and of D_{band+1}
 };
 
 // Mel band energies of one frame, mfcc.js:40-62: E_j = sum_k w_jk p_k, p_k = a_k^2 (float32).
@@ -850,39 +854,31 @@ struct MelTab {
 // segment j+1). So E_j = U_j + D_{j+1} with U_m = sum_{k in m} up(k) p_k and
 // D_m = sum_{k in m} dn(k) p_k: two segmented sums over the bins, computed as in-lane
 // runs plus one segmented scan across the lanes. Where the segments start
-// does not depend on the frame, so every branch of that logic is a plan table (MelTab):
-// per bin a keep factor (0 restarts the sums) and the scratch slot the running sums are
-// stored to, per lane the keeps of the six scan steps and the slots of the head and tail
-// totals. No selects: per bin a packed multiply and a packed FMA, per scan step two DPP
-// moves and a packed FMA. No cross-segment sums are formed, so there is no cancellation;
-// the sums are float32 like the reference's Float32Array accumulation, in a different order
-// (and the falling weight is 1 - rising in float32, within an ulp of the f64 ratio).
+// does not depend on the frame, so every branch of that logic is a plan table (MelTab,
+// plan.cpp mel_lane_tables): per bin the weight pair and a keep factor (0 restarts the sums),
+// per lane the keeps of the six scan steps and, per band, where its two segment totals end up.
+// Each lane stores its running sums before bins 1..R-1 at fixed entries of the slot buffer
+// (immediate offsets: no per-bin address), then the scan's carry into it; band j sums
+// carry-or-zero + entry for U_j and D_{j+1}. No selects: per bin a packed multiply and a packed
+// FMA, per scan step two DPP moves and a packed FMA. No cross-segment sums are formed, so there
+// is no cancellation; the sums are float32 like the reference's Float32Array accumulation, in a
+// different order (and the falling weight is 1 - rising in float32, within an ulp of the f64 ratio).
 template <int N>
 __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>::R], int lane, float2* buf,
                                              FrameRec& rec, const MelTab<N>& mt) {
   constexpr int R = Geo<N>::R;
   const int nf = ap->nfilt;
-  float2* mud = buf;  // (U, D) of segments 0..nf+1, then the 64 head partials (kMelHead)
   wave_sync();  // band-sum reads of the prefix buffer are done
-  float2* mine = mud + lane;  // segment slot `lane` (and lane + 64), head slot kMelHead + lane
-  // Every segment with a bin is stored by the scan below; only an empty one (b_m = b_{m+1},
-  // 40 bands at N = 512 for example) needs its slot zeroed first (plan flag, one LDS round trip)
-  if (ap->mel_zero) {
-    if (lane < nf + 2) mine[0] = make_float2(0.0f, 0.0f);
-    if (lane + 64 < nf + 2) mine[64] = make_float2(0.0f, 0.0f);
-    wave_sync();
-  }
+  float2* mine = buf + lane;
   f32x2 acc = {0.0f, 0.0f};
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) {
     const float p = av[jj] * av[jj];  // powerSpectrum.js
-    mud[mt.slot(jj)] = make_float2(acc.x, acc.y);
-    const float up = mt.rise(jj), kp = mt.keep(jj);
-    const f32x2 w = {up, 1.0f - up}, pp = {p, p}, kk = {kp, kp};
+    if (jj > 0) mine[(jj - 1) * 64] = make_float2(acc.x, acc.y);
+    const float kp = mt.keep(jj);
+    const f32x2 w = mt.weights(jj), pp = {p, p}, kk = {kp, kp};
     acc = __builtin_elementwise_fma(w, pp, acc * kk);
   }
-  // segmented inclusive scan of the lane tails: s += keep_s * s_src (keep_s = 0 once the
-  // lanes summed so far hold a segment start; a missing source lane reads 0)
   f32x2 sc = acc;
   auto step = [&](float u, float d, int s) {
     const f32x2 src = {u, d}, ks = {mt.scan_keep(s), mt.scan_keep(s)};
@@ -894,12 +890,18 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
   step(dpp_f<0x118>(sc.x), dpp_f<0x118>(sc.y), 3);  // row_shr:8
   step(dpp_f<0x142, 0xA>(sc.x), dpp_f<0x142, 0xA>(sc.y), 4);  // row_bcast:15 (rows 1, 3)
   step(dpp_f<0x143, 0xC>(sc.x), dpp_f<0x143, 0xC>(sc.y), 5);  // row_bcast:31 (rows 2, 3)
-  const float xu = dpp_f<0x138>(sc.x), xd = dpp_f<0x138>(sc.y);  // exclusive: carry into this lane (wave_shr:1)
-  const float2 hp = mine[kMelHead];
-  mud[mt.head_slot()] = make_float2(xu + hp.x, xd + hp.y);  // the segment this lane's first start closes
-  mud[mt.tail_slot()] = make_float2(sc.x, sc.y);           // lane 63: the segment still open at the last bin
+  const float xu = dpp_f<0x138>(sc.x), xd = dpp_f<0x138>(sc.y);  // exclusive: carry into this lane
+  mine[(R - 1) * 64] = make_float2(xu, xd);
+  if (lane == 63) buf[R * 64] = make_float2(sc.x, sc.y);
+  if (lane == 0) buf[R * 64 + 1] = make_float2(0.0f, 0.0f);
   wave_sync();
-  if (lane < nf) rec.lm[lane] = mine[0].x + mine[1].y;  // nf <= kMaxMel = 64
+  if (lane < nf) {  // nf <= kMaxMel = 64
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(buf);
+    const uint32_t u = mt.asm_u(), d = mt.asm_d();
+    const float U = reinterpret_cast<const float2*>(b + (u & 0xFFFFu))->x + reinterpret_cast<const float2*>(b + (u >> 16))->x;
+    const float D = reinterpret_cast<const float2*>(b + (d & 0xFFFFu))->y + reinterpret_cast<const float2*>(b + (d >> 16))->y;
+    rec.lm[lane] = U + D;
+  }
 }
 
 // float32 bits of 2^64: an amplitude a >= 2^64 has a * a = +inf in float32 (a < 2^64 stays

@@ -11,7 +11,6 @@ constexpr int kMaxMel = 64;
 constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
-constexpr int kMelHead = kMaxMel + 2;  // mel scratch: segment sums [0, nfilt + 2), head partials from here
 // Mel band chains in the reference's own order (MGX_FLAG_MFCC_REFERENCE, every N): F frames x
 // nfilt chains on 64 / F packed tracks (F = 8 for nfilt <= 31, else F = 4; plan.cpp chain_schedule).
 constexpr int kRecBytes = 520;  // sizeof(FrameRec) (kernels.hip)
@@ -21,7 +20,11 @@ constexpr int kChainMaxN = 2048;
 constexpr int kChainSkip = 1 << 30;  // FrameRec.zcr flag bit: a non-finite frame keeps its phase-1 mel sums
 // dwords of one lane's mel record for R bins per lane (R weights, R slot bytes, R keep bytes,
 // 8 bytes of scan keeps and slots), padded to whole 16-byte loads
-__host__ __device__ constexpr int mel_rec_words(int R) { return (R + 2 * ((R + 3) / 4) + 2 + 3) / 4 * 4; }
+// The lane's mel record (plan.cpp mel_lane_tables): the bin weights -- (rise, 1 - rise) pairs
+// up to R = 8 slots per lane, the rising weight alone above --, the keep bytes, the scan keeps
+// (2 words) and the four assembly offsets (2 words).
+__host__ __device__ constexpr int mel_weight_words(int R) { return R <= 8 ? 2 * R : R; }
+__host__ __device__ constexpr int mel_rec_words(int R) { return (mel_weight_words(R) + (R + 3) / 4 + 4 + 3) / 4 * 4; }
 // Device-resident, read-only tables of a plan (one allocation, see plan.cpp).
 struct DevTables {
   const float* window;       // N, the selected window (src/meyda.js:116-138)
@@ -60,7 +63,6 @@ struct KernelArgs {
   int need_energy;       // rms or energy: the wave sum of the squares (SUB kernel)
   int need_zcr;          // zcr: the sign-change ballots (SUB kernel)
   int dct_sequential;    // MGX_FLAG_DCT_SEQUENTIAL: the DCT as VALU FMAs in the reference's order
-  int mel_zero;          // some mel segment [b_m, b_{m+1}) is empty: the scan's slots are zeroed first
   int wg_ranks;          // workgroups per CU when the grid is the resident one (else 1): their work shares
   int chain_groups;      // 8-step groups of the mel chain tracks (0: the segmented scan)
   int chain_pair;        // the chains of two consecutive batches of a wave run together (8 frames, nfilt <= 31)

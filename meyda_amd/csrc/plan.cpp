@@ -232,46 +232,74 @@ void mel_segments(const int32_t* b, int nf, int L, std::vector<float>& wud, std:
 
 // Per-lane form of the segment tables for kernels.hip mel_energies (lane t owns bins
 // [R t, R t + R), R = L / 64), one record of mgx::mel_rec_words(R) dwords per lane:
-//   R floats      rising weight of each bin (the falling one is 1 - rising in the kernel)
-//   R bytes       the scratch slot the running sums are stored to before the bin is added
+//   weights       per bin the rising weight and, up to R = 8, the falling one 1 - rising in
+//                 float32 as a pair (the kernel forms it itself above)
 //   R bytes       keep (1, or 0 where a segment starts: the sums restart)
-//   8 bytes       keeps (0/1) of the 6 segmented-scan steps, head-total slot, tail slot
-// Slots index float2 (U, D) entries of the wave's mel scratch: 0..nf+1 the segments (nf+1
-// collects the bins of no band, and bin -1), kMelHead + t the head partial of lane t. Up
-// to and including the lane's first segment start the sums go to the lane's head slot (the
-// last of these stores is the lane's partial of the segment that began in an earlier lane,
-// completed with the carry of the segmented scan), afterwards to that segment's slot (final
-// at the start that closes it, a running partial that a later store overwrites otherwise;
-// only this lane stores there in the loop, so lanes inside one long segment never store to
-// one address together). The scan keeps replay the flag logic of a Hillis-Steele segmented
-// scan over the kernel's DPP steps (row_shr 1, 2, 4, 8; row_bcast 15 on rows 1, 3;
-// row_bcast 31 on rows 2, 3), which depends only on which lanes hold a segment start.
+//   8 bytes       keeps (0/1) of the 6 segmented-scan steps
+//   2 words       the assembly offsets of band t (below)
+// Dense layout of the wave's slot buffer (float2 (U, D) entries): lane t stores its running sums
+// before bin jj >= 1 at entry (jj - 1) * 64 + t (fixed offsets, no per-bin address), the segmented
+// scan's carry into it at (R - 1) * 64 + t, lane 63 the segment still open at the last bin at
+// R * 64 and lane 0 a zero at R * 64 + 1. Segment m's total is carry-or-zero + entry: the running
+// sum before the bin that starts the next segment (or the zero when that bin opens a lane), plus
+// the carry into that lane when m began in an earlier lane; lane 63's inclusive scan value when m
+// is open at the last bin; 0 when m has no bin. Band j (lane j < nf) sums U_j and D_{j+1} from the
+// byte offsets (cU | dU << 16, cD | dD << 16). The scan keeps replay the flag logic of a
+// Hillis-Steele segmented scan over the kernel's DPP steps (row_shr 1, 2, 4, 8; row_bcast 15 on
+// rows 1, 3; row_bcast 31 on rows 2, 3), which depends only on which lanes hold a segment start.
 void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& wud, int nf, int L,
                      std::vector<uint32_t>& rec) {
-  const int R = L / 64, sink = nf + 1, W = mgx::mel_rec_words(R);
+  const int R = L / 64, sink = nf + 1, W = mgx::mel_rec_words(R), B = (R + 3) / 4, WW = mgx::mel_weight_words(R);
   rec.assign((size_t)W * 64, 0u);
+  const uint32_t zero = 8u * (uint32_t)(R * 64 + 1), tail = 8u * (uint32_t)(R * 64);
   bool seen[64];
   for (int t = 0; t < 64; ++t) {
     uint32_t* r = &rec[(size_t)W * t];
-    uint8_t* slots = reinterpret_cast<uint8_t*>(r + R);
-    uint8_t* keeps = slots + 4 * ((R + 3) / 4);
-    uint8_t* lane8 = keeps + 4 * ((R + 3) / 4);
+    uint8_t* keeps = reinterpret_cast<uint8_t*>(r + WW);
     seen[t] = false;
-    int hseg = sink;
     for (int jj = 0; jj < R; ++jj) {
       const int k = R * t + jj;
       const int prevseg = k == 0 ? sink : seg[k - 1];
       const bool start = seg[k] != prevseg;
-      slots[jj] = (uint8_t)(seen[t] ? prevseg : mgx::kMelHead + t);
-      if (start && !seen[t]) {
-        seen[t] = true;
-        hseg = prevseg;
-      }
+      if (start) seen[t] = true;
       keeps[jj] = start ? 0 : 1;
-      memcpy(&r[jj], &wud[2 * k], 4);
+      if (WW == 2 * R) {  // (rise, 1 - rise): the falling weight the kernel would form, in float32
+        const float up = wud[2 * k], dn = 1.0f - up;
+        memcpy(&r[2 * jj], &up, 4);
+        memcpy(&r[2 * jj + 1], &dn, 4);
+      } else {
+        memcpy(&r[jj], &wud[2 * k], 4);
+      }
     }
-    lane8[6] = (uint8_t)(seen[t] ? hseg : mgx::kMelHead + t);
-    lane8[7] = (uint8_t)(t == 63 ? seg[L - 1] : mgx::kMelHead + t);
+  }
+  // (carry-or-zero, entry) byte offsets of segment m's total
+  auto total = [&](int m, uint32_t& c, uint32_t& d) {
+    int first = -1, last = -1;
+    for (int k = 0; k < L; ++k)
+      if (seg[k] == m) {
+        if (first < 0) first = k;
+        last = k;
+      }
+    c = d = zero;
+    if (first < 0) return;           // an empty segment: 0
+    const int next = last + 1;
+    if (next == L) {                 // open at the last bin: lane 63's inclusive scan value
+      d = tail;
+      return;
+    }
+    const int e = next / R, pos = next % R;
+    if (first < e * R) c = 8u * (uint32_t)((R - 1) * 64 + e);  // started in an earlier lane: + its carry
+    if (pos > 0) d = 8u * (uint32_t)((pos - 1) * 64 + e);       // the running sum before the next start
+  };
+  for (int j = 0; j < 64; ++j) {
+    uint32_t cU = zero, dU = zero, cD = zero, dD = zero;
+    if (j < nf) {
+      total(j, cU, dU);
+      total(j + 1, cD, dD);
+    }
+    uint32_t* r = &rec[(size_t)W * j];
+    r[WW + B + 2] = cU | dU << 16;
+    r[WW + B + 3] = cD | dD << 16;
   }
   bool f[64];
   for (int t = 0; t < 64; ++t) f[t] = seen[t];
@@ -283,7 +311,7 @@ void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& 
       if (s < 4) src = (t % 16) >= (1 << s) ? t - (1 << s) : -1;
       else if (s == 4) src = (row == 1 || row == 3) ? row * 16 - 1 : -1;
       else src = (row == 2 || row == 3) ? 31 : -1;
-      uint8_t* lane8 = reinterpret_cast<uint8_t*>(&rec[(size_t)W * t + R]) + 8 * ((R + 3) / 4);
+      uint8_t* lane8 = reinterpret_cast<uint8_t*>(&rec[(size_t)W * t + WW + B]);
       lane8[s] = f[t] ? 0 : 1;
       g[t] = f[t] || (src >= 0 && f[src]);
     }
@@ -418,7 +446,6 @@ struct mgx_plan {
   double freq_sum = 0, pow_freq_sum = 0, nyq = 0, sharp_tail = 0;
   int grid_cap = 1;
   int cus = 0;  // compute units of the plan's device
-  int mel_zero = 1;  // some mel segment is empty (kernels.hip mel_energies)
   int chain_groups = 0;  // MGX_FLAG_MFCC_REFERENCE: 8-step groups of the mel chains (chain_schedule)
   int chain_pair = 0;  // ... over two consecutive batches of a wave (8 frames)
   // the mel chains' power-row rings (kernels.hip KGeo::GROWS), one per stream a launch used: the
@@ -561,9 +588,6 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
 
   auto* p = new mgx_plan();
   p->d = *d;
-  p->mel_zero = 0;
-  for (int m = 0; m <= nf; ++m)
-    if (bins[m] >= bins[m + 1]) p->mel_zero = 1;
   p->n = n;
   p->L = L;
   // spectralSlope.js:9-16 input-independent sums, in the reference's order
@@ -679,7 +703,6 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.ncoef = (int)p->d.num_mfcc_coeffs;
   a.scalar_f64 = (int)p->d.scalar_f64;
   a.dct_sequential = (p->d.flags & MGX_FLAG_DCT_SEQUENTIAL) ? 1 : 0;
-  a.mel_zero = p->mel_zero;
   a.chain_groups = p->chain_groups;
   a.chain_pair = p->chain_pair;
   bool spec = o->loudness_specific || o->mfcc || o->amplitude_spectrum || o->power_spectrum || o->complex_real;
