@@ -702,6 +702,13 @@ struct FrameRec {
   float sharp_sum;
 };
 
+// Record fb (< 4) of the wave's batch and small per-lane offsets by 24-bit multiplies: the lane
+// indices come through opaque() (no range the compiler can see), and a 32-bit v_mul_lo_u32 /
+// 64-bit v_mad_u64_u32 is a multi-pass instruction where v_mul_u32_u24 is one VALU op.
+__device__ __forceinline__ FrameRec& rec_at(FrameRec* recs, int fb) {
+  return *reinterpret_cast<FrameRec*>(reinterpret_cast<unsigned char*>(recs) + __umul24((unsigned)fb, (unsigned)sizeof(FrameRec)));
+}
+
 // Math.pow(x, 0.23) rounded to float32 (loudness.js:62), without the f64 exp/log
 // routines: x = m 2^e with m in [1, 2); log2 m = log2(m_hi) + m_lo / (m_hi ln 2) from the
 // f32 hardware log (m_hi = (float)m); y = 0.23 log2 x in double; 2^y = 2^floor(y) 2^frac(y)
@@ -888,8 +895,10 @@ __device__ __forceinline__ void mel_energies(KArgs* ap, const float (&av)[Geo<N>
   step(dpp_f<0x112>(sc.x), dpp_f<0x112>(sc.y), 1);  // row_shr:2
   step(dpp_f<0x114>(sc.x), dpp_f<0x114>(sc.y), 2);  // row_shr:4
   step(dpp_f<0x118>(sc.x), dpp_f<0x118>(sc.y), 3);  // row_shr:8
-  step(dpp_f<0x142, 0xA>(sc.x), dpp_f<0x142, 0xA>(sc.y), 4);  // row_bcast:15 (rows 1, 3)
-  step(dpp_f<0x143, 0xC>(sc.x), dpp_f<0x143, 0xC>(sc.y), 5);  // row_bcast:31 (rows 2, 3)
+  // (the row broadcasts write every row: the rows a step must not add to have keep 0 in the plan,
+  // so no zero has to be written ahead of a row-masked move)
+  step(dpp_f<0x142>(sc.x), dpp_f<0x142>(sc.y), 4);  // row_bcast:15 (rows 1, 3)
+  step(dpp_f<0x143>(sc.x), dpp_f<0x143>(sc.y), 5);  // row_bcast:31 (rows 2, 3)
   const float xu = dpp_f<0x138>(sc.x), xd = dpp_f<0x138>(sc.y);  // exclusive: carry into this lane
   mine[(R - 1) * 64] = make_float2(xu, xd);
   if (lane == 63) buf[R * 64] = make_float2(sc.x, sc.y);
@@ -1106,13 +1115,15 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   } else {
     // the 64 lane partials summed in float32 too (6 DPP-fused adds instead of 6 f64 DPP
     // steps): ~4e-7 relative at most on top of the partials' own ~1e-6, against the 1e-5 bar
+    // (only lane 63 is read: the row broadcasts need no row mask -- rows that should not add get
+    // values nobody reads -- so no zero has to be written ahead of them)
     float t = e32;
     t += dpp_f<0xB1>(t);
     t += dpp_f<0x4E>(t);
     t += dpp_f<0x141>(t);
     t += dpp_f<0x140>(t);
-    t += dpp_f<0x142, 0xA>(t);
-    t += dpp_f<0x143, 0xC>(t);
+    t += dpp_f<0x142>(t);
+    t += dpp_f<0x143>(t);
     e = (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
   }
   if (lane == 0) {
@@ -1431,7 +1442,9 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       rec.band[lane] = pbuf[blim >> 16] - pbuf[blim & 0xFFFFu];
     } else {
       const int lb = opaque(lane);  // (an address kept live across the frame loop spills at N = 2048)
-      rec.band[lb] = pbuf[pd(klim[lb + 1])] - pbuf[pd(klim[lb])];  // limits staged in LDS
+      // limits staged in LDS as byte offsets of their prefix-row entries (pd(lim) * 8)
+      const unsigned char* pb = reinterpret_cast<const unsigned char*>(pbuf);
+      rec.band[lb] = *reinterpret_cast<const double*>(pb + klim[lb + 1]) - *reinterpret_cast<const double*>(pb + klim[lb]);
     }
   }
   if (lane == 0) {
@@ -1628,8 +1641,8 @@ __device__ __forceinline__ void mfcc_log(KArgs* q, int l2, FrameRec* recs, int l
     return band < nfilt ? (ref_log ? (float)log((double)v) : ln_f32(v)) : 0.0f;  // padding for dct_sum
   };
   for (int i = l2; i < FPW * (nfp / 2); i += 64) {
-    const int fb = i % FPW, band = 2 * (i / FPW);
-    f32x2* pp = reinterpret_cast<f32x2*>(&recs[fb].lm[lmo + band]);
+    const int fb = i & (FPW - 1), band = 2 * (int)((unsigned)i / FPW);  // (i >= 0: unsigned division)
+    f32x2* pp = reinterpret_cast<f32x2*>(&rec_at(recs, fb).lm[lmo + band]);
     const f32x2 v = *pp;
     *pp = f32x2{ln1(v.x, band), ln1(v.y, band + 1)};
   }
@@ -1646,7 +1659,7 @@ __device__ __forceinline__ void mfcc_dct(KArgs* q, int l2, FrameRec* recs, const
     // sequential order, one lane per (coefficient, frame). (The matrix-core form below is the
     // default: 0.5 % faster for the whole kernel and equal on every golden coefficient)
     for (int i = l2; i < FPW * nc; i += 64) {
-      const int c = i / FPW, fb = i % FPW;
+      const int c = (int)((unsigned)i / FPW), fb = i & (FPW - 1);
       const uint64_t f = fbase + fb;
       const double v = dct_sum(dct_lds, recs[fb].lm + lmo, c, nc, nfilt);
       if (f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)div_by(v, nc, q->rcp_ncoef);
@@ -1662,21 +1675,24 @@ __device__ __forceinline__ void mfcc_dct(KArgs* q, int l2, FrameRec* recs, const
   // frame l & 3. The products of two floats are exact in double, as in the reference; only the f64
   // summation order differs.
   static_assert(FPW == 4, "one 4 x 4 block column per frame of the batch");
-  const int kk = l2 >> 4, fa = l2 & 3, nsteps = (nfilt + 3) >> 2;
-  const float* lmrow = recs[fa].lm + lmo;
+  const int kk = (l2 >> 4) & 3, fa = l2 & 3, nsteps = (nfilt + 3) >> 2;
+  const float* lmrow = rec_at(recs, fa).lm + lmo;
+  // the batch's mfcc rows from a wave-uniform base (scalar 64-bit arithmetic), lanes at 24-bit offsets
+  const auto mrow = q->out.mfcc ? uniform_ptr(gbl(q->out.mfcc) + fbase * (uint64_t)nc) : nullptr;
   for (int mt = 0; mt < nc; mt += 16) {
     // (a tile row past the last coefficient reads the last row again instead of a guarded zero:
     // a row of A only feeds its own coefficient's outputs, never stored)
     const int ca = min(mt + (l2 & 15), nc - 1);
+    const float* dcol = dct_lds + ca + __umul24((unsigned)kk, (unsigned)nc);  // row n = 4 st + kk
     double acc = 0.0;
     for (int st = 0; st < nsteps; ++st) {
       const int n = 4 * st + kk;  // < nfilt rounded up to 8: the tables are zero-padded
-      const float av = dct_lds[ca + n * nc];
+      const float av = dcol[__umul24((unsigned)(4 * st), (unsigned)nc)];
       acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)av, (double)lmrow[n], acc, 0, 0, 0);
     }
     const int c = mt + 4 * ((l2 >> 2) & 3) + kk;
     const uint64_t f = fbase + fa;
-    if (c < nc && f < q->num_frames && q->out.mfcc) gbl(q->out.mfcc)[f * nc + c] = (float)div_by(acc, nc, q->rcp_ncoef);
+    if (c < nc && f < q->num_frames && mrow) mrow[__umul24((unsigned)fa, (unsigned)nc) + c] = (float)div_by(acc, nc, q->rcp_ncoef);
   }
 }
 
@@ -1733,7 +1749,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     void** kptr = reinterpret_cast<void**>(smem + LY::kc_off);
     int* klim = reinterpret_cast<int*>(smem + LY::kc_off + 16 * 8);
     if (threadIdx.x < MGX_NUM_SCALARS) kptr[threadIdx.x] = ap->out.scalars[threadIdx.x];
-    if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = gbl(ap->t.bblim)[threadIdx.x - 64];
+    // the bark limits as byte offsets of their entries in the padded prefix row (band sums)
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = 8 * pd(gbl(ap->t.bblim)[threadIdx.x - 64]);
   }
   if constexpr (Geo<N>::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
     stage_twiddles<N, 1, 0>(reinterpret_cast<double2*>(smem + LY::twl_off), gbl(ap->t.tw), gbl(ap->t.twm));
@@ -1837,9 +1854,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // the band lane's prefix-row offsets pd(lim[b]) | pd(lim[b + 1]) << 16 (G::BLIM_REG)
   uint32_t blim = 0;
   if constexpr (G::BLIM_REG) {
-    const int* kl = reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8);
+    const int* kl = reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8);  // 8 pd(lim)
     const int lb = lane < kBark ? lane : 0;
-    blim = (uint32_t)pd(kl[lb]) | ((uint32_t)pd(kl[lb + 1]) << 16);
+    blim = (uint32_t)(kl[lb] >> 3) | ((uint32_t)(kl[lb + 1] >> 3) << 16);
   }
   float wreg[CH];
   if constexpr (G::WIN_REG) {
@@ -1907,17 +1924,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         // lane's pair sum is the reduction tree's first level and the four row steps the rest,
         // so every partial sum is the one the 32-lane layout formed (same results).
         static_assert(FPW * 16 == 64, "one DPP row per frame of the batch");
-        const int fb = l2 >> 4, pr = l2 & 15;
+        const int fb = (l2 >> 4) & 3, pr = l2 & 15;
         const uint64_t f = f0 + fb;
         const bool live = pr < kBark / 2;
         const int b0 = live ? 2 * pr : 0;
-        const double sum0 = recs[fb].band[b0], sum1 = recs[fb].band[b0 + 1];
+        FrameRec& rb = rec_at(recs, fb);
+        const double sum0 = rb.band[b0], sum1 = rb.band[b0 + 1];
         // loudness.js:62 Math.pow(sum, 0.23), stored to Float32Array
         float sp0 = pow023(sum0), sp1 = pow023(sum1);
         if (!live) sp0 = sp1 = 0.0f;
         if (live && f < q->num_frames && q->out.loudness_specific)
-          *reinterpret_cast<__attribute__((address_space(1))) f32x2*>(gbl(q->out.loudness_specific) + f * kBark + b0) =
-              f32x2{sp0, sp1};
+          *reinterpret_cast<__attribute__((address_space(1))) f32x2*>(uniform_ptr(gbl(q->out.loudness_specific) + f0 * kBark) +
+                                                                     __umul24((unsigned)fb, (unsigned)kBark) + b0) = f32x2{sp0, sp1};
         // loudness.js:67-69 total; perceptualSpread.js:7-12 max; perceptualSharpness.js:7-14
         // (off-by-one spec[i+1] for i < 15, then the constant 0.066 e^{0.171 (i+1)} tail).
         // total in double (perceptualSpread's (total - max) cancels); max exact in float32;
@@ -1934,9 +1952,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         // (every lane of the row holds the frame's sums; the three quotients are formed in the
         // scalar step below, with the others)
         if (pr == 15) {
-          recs[fb].band[0] = tot;
-          recs[fb].loud_max = mx;
-          recs[fb].sharp_sum = sh;
+          rb.band[0] = tot;
+          rb.loud_max = mx;
+          rb.sharp_sum = sh;
         }
       }
       MGX_MARK(loud2_done);
@@ -1958,11 +1976,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       // the scalar features: one lane per (feature, frame); the loudness total, perceptual
       // spread and sharpness from the loudness step's record entries (16 x 4 lanes at most)
       for (int i = l2; i < (MGX_PERCEPTUAL_SHARPNESS + 1) * FPW; i += 64) {
-        const int sc = i / FPW, fb = i % FPW;
+        const int sc = (int)((unsigned)i / FPW), fb = i & (FPW - 1);
         const uint64_t f = f0 + fb;
         void* dst = reinterpret_cast<void* const*>(smem + LY::kc_off)[sc];
         if (f >= q->num_frames || dst == nullptr) continue;
-        const double v = scalar_value<N, SUB>(q, recs[fb], sc);
+        const double v = scalar_value<N, SUB>(q, rec_at(recs, fb), sc);
         if (q->scalar_f64) gbl(static_cast<double*>(dst))[f] = v;
         else gbl(static_cast<float*>(dst))[f] = (float)v;
       }

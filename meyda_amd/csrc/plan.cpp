@@ -312,7 +312,9 @@ void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& 
       else if (s == 4) src = (row == 1 || row == 3) ? row * 16 - 1 : -1;
       else src = (row == 2 || row == 3) ? 31 : -1;
       uint8_t* lane8 = reinterpret_cast<uint8_t*>(&rec[(size_t)W * t + WW + B]);
-      lane8[s] = f[t] ? 0 : 1;
+      // 0 also where the step has no source for this lane: the kernel's row broadcasts write
+      // every row (no row mask), so a row outside the step's rows must not add what it receives
+      lane8[s] = (f[t] || src < 0) ? 0 : 1;
       g[t] = f[t] || (src >= 0 && f[src]);
     }
     memcpy(f, g, sizeof f);
