@@ -5,7 +5,7 @@ costs of tools/ubench/op_rates (profiles/r01_op_rates.log) into an estimate of t
 busy fraction. Writes profiles/pmc_valu.json (a report; bench.py takes its own counters live).
 Counter durations under PMC collection are not used: the busy estimate divides by the
 kernel time measured without the profiler (the launch duration of the committed bench line,
-profiles/r03_bench.log)."""
+profiles/r04_bench.log)."""
 import collections
 import csv
 import glob
@@ -34,7 +34,7 @@ def main():
     valu = per["SQ_INSTS_VALU"]
     known = sum(per.get(k, 0.0) for k in COST)
     cycles = sum(per.get(k, 0.0) * c for k, c in COST.items()) + (valu - known) * OTHER
-    bench = json.loads(open(os.path.join(ROOT, "profiles/r03_bench.log")).read().strip().splitlines()[-1])
+    bench = json.loads(open(os.path.join(ROOT, "profiles/r04_bench.log")).read().strip().splitlines()[-1])
     kms = bench["roofline"]["kernel_ms"]
     frame_cycles = kms * 1e-3 * 2.4e9 * 1024 / F  # SIMD cycles per frame: 1,024 SIMDs at 2.4 GHz (GRBM_GUI_ACTIVE)
     f64 = sum(per.get(k, 0.0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
