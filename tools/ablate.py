@@ -80,7 +80,10 @@ PATCHES = {
                ("      if (tame) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);",
                 "      if (opaque(0)) run_passes<N, 1, FAITH, true, TWL>(v, lpf, buf, tw, twf, twm, twl);"),
                ("      else run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);",
-                "      else if (opaque(0)) run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);")],
+                "      else if (opaque(0)) run_passes<N, 1, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);"),
+               # (the fast precision's f32 passes)
+               ("      run_passes<N, 0, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);",
+                "      if (opaque(0)) run_passes<N, 0, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);")],
     # two workgroup barriers per frame at the mel step (the cost of synchronising the workgroup's
     # four waves once per frame; timing only, the batch size must give every wave the same count)
     "bar2": [("  MGX_MARK(bands_done);\n", "  MGX_MARK(bands_done);\n  if (!CHAIN) { lds_barrier(); lds_barrier(); }\n")],

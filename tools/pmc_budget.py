@@ -27,6 +27,7 @@ def run(specs):
     n = int(os.environ.get("PROBE_N", "1024"))
     x = torch.empty(F, n, dtype=torch.float32, device="cuda")
     capi.synth_frames_device(x, 0x6D657964)
+    prec = os.environ.get("PROBE_PRECISION", "faithful")  # "fast": the f32-butterfly kernels
     plan0 = capi.Plan(buffer_size=n)
     _, o = plan0.alloc_outputs(F, capi.ALL_FEATURES)
     s = torch.cuda.current_stream()
@@ -37,7 +38,7 @@ def run(specs):
             path, fl = path.split(":", 1)
             flags = int(fl, 0)
         L = load(capi.LIB_PATH if path == "base" else os.path.join(ROOT, path))
-        d = capi.make_desc(buffer_size=n)
+        d = capi.make_desc(buffer_size=n, precision=prec)
         d.flags = flags
         h = ctypes.c_void_p()
         assert L.mgx_plan_create(ctypes.byref(d), ctypes.byref(h)) == 0, name
@@ -61,7 +62,11 @@ def report(d, names):
                 per[cn][names[vi]].append(v)
     cols = sorted(per)
     print("# per frame (counter sum over the dispatch / 262,144 frames; SQ_INSTS_* count wave instructions)")
-    print("%-22s" % "variant" + "".join("%11s" % c.replace("SQ_INSTS_", "").replace("SQ_", "")[:10] for c in cols))
+    def short(c):  # unique column names of at most 10 characters
+        for a, b in (("SQ_INSTS_VALU_", "V_"), ("SQ_INSTS_", ""), ("SQ_ACTIVE_INST_", "ACT_"), ("SQ_WAIT_INST_", "WAITI_"), ("SQ_", "")):
+            c = c.replace(a, b)
+        return c.replace("_CYCLES", "_CYC")[:10]
+    print("%-22s" % "variant" + "".join("%11s" % short(c) for c in cols))
     for nm in names:
         vals = []
         for c in cols:
