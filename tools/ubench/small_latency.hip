@@ -1,0 +1,114 @@
+// Where a one-frame host call's time goes (the real-time path, plan.cpp extract_host_small):
+// the extraction launched on device-mapped pinned host buffers, then
+//   A  hipStreamSynchronize (what extract_host_small does),
+//   B  a host spin on the mapped output words (sentinel bits -> value), then the stream sync,
+//   C  an empty kernel + hipStreamSynchronize (the launch and wake-up floor),
+//   D  the kernel's own duration between two events.
+// Build: hipcc --offload-arch=gfx950 -O2 -I include -o tools/ubench/small_latency tools/ubench/small_latency.hip \
+//          -L meyda_amd -lmeyda_gpu -Wl,-rpath,$PWD/meyda_amd
+// usage: small_latency [N] [calls]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "meyda_gpu.h"
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+__global__ void empty_kernel() {}
+
+static double now_us() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static double median(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 512;
+  const int calls = argc > 2 ? atoi(argv[2]) : 2000;
+  mgx_plan_desc d;
+  mgx_plan_desc_init(&d);
+  d.buffer_size = (uint32_t)n;
+  mgx_plan* p = nullptr;
+  if (mgx_plan_create(&d, &p) != MGX_OK) {
+    fprintf(stderr, "plan: %s\n", mgx_last_error());
+    return 1;
+  }
+  float *hin, *hout, *din, *dout;
+  CK(hipHostMalloc((void**)&hin, n * sizeof(float), hipHostMallocMapped | hipHostMallocCoherent));
+  CK(hipHostMalloc((void**)&hout, 256, hipHostMallocMapped | hipHostMallocCoherent));
+  CK(hipHostGetDevicePointer((void**)&din, hin, 0));
+  CK(hipHostGetDevicePointer((void**)&dout, hout, 0));
+  for (int i = 0; i < n; ++i) hin[i] = (float)((i * 7919) % 2001 - 1000) / 1000.0f;
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  mgx_outputs o;
+  memset(&o, 0, sizeof(o));
+  o.scalars[MGX_RMS] = dout;
+  o.scalars[MGX_SPECTRAL_CENTROID] = dout + 16;
+  volatile uint32_t* w0 = reinterpret_cast<volatile uint32_t*>(hout);
+  volatile uint32_t* w1 = reinterpret_cast<volatile uint32_t*>(hout + 16);
+  const uint32_t kSentinel = 0xFFBADBADu;  // a NaN payload the kernel never writes for finite input
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<double> ta, tb, tc, td, tl;
+  for (int it = 0; it < calls + 50; ++it) {
+    // A: launch + stream synchronise
+    double t0 = now_us();
+    if (mgx_extract_device(p, din, 1, &o, s) != MGX_OK) return 1;
+    double t1 = now_us();
+    CK(hipStreamSynchronize(s));
+    double t2 = now_us();
+    // B: launch + spin on the mapped outputs, then the stream sync (outside the time)
+    *w0 = kSentinel;
+    *w1 = kSentinel;
+    double t3 = now_us();
+    if (mgx_extract_device(p, din, 1, &o, s) != MGX_OK) return 1;
+    while (*w0 == kSentinel || *w1 == kSentinel) {
+    }
+    double t4 = now_us();
+    CK(hipStreamSynchronize(s));
+    // C: empty kernel
+    double t5 = now_us();
+    empty_kernel<<<1, 64, 0, s>>>();
+    CK(hipStreamSynchronize(s));
+    double t6 = now_us();
+    // D: kernel duration
+    CK(hipEventRecord(e0, s));
+    if (mgx_extract_device(p, din, 1, &o, s) != MGX_OK) return 1;
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (it >= 50) {
+      ta.push_back(t2 - t0);
+      tl.push_back(t1 - t0);
+      tb.push_back(t4 - t3);
+      tc.push_back(t6 - t5);
+      td.push_back(ms * 1e3);
+    }
+  }
+  printf("{\"n\": %d, \"calls\": %d, \"launch_sync_us\": %.2f, \"launch_call_us\": %.2f, \"launch_spin_us\": %.2f, "
+         "\"empty_kernel_sync_us\": %.2f, \"kernel_event_us\": %.2f, \"rms\": %.9g, \"centroid\": %.9g}\n",
+         n, calls, median(ta), median(tl), median(tb), median(tc), median(td), hout[0], hout[16]);
+  mgx_plan_destroy(p);
+  return 0;
+}
