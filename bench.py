@@ -378,8 +378,11 @@ def run_mode(step, devs, steps, warmup, dist):
     synchronisation on both sides, pipelined over two streams (pipelined()); HIP events on the
     launch stream around the whole timed region give the launch period (no events between the
     steps: an event pair per step cost 1-2 % of the step time, tools/step_overlap.py). Then an
-    untimed single-stream pass with an event pair around each launch: the launch duration on
-    its own, which is what rocprofv3 reports per dispatch."""
+    untimed single-stream pass with an event pair around each launch (the spread of single
+    launches), and one more of 20 launches back to back on one stream with one event pair around
+    them all: the mean launch duration (plus the small dispatch gap between serialised launches),
+    which is what rocprofv3 reports per dispatch -- an event pair around every launch adds its own
+    marker packets to each (~4 % of a 0.6 ms launch against the profiler's durations)."""
     d0 = devs.devs[0]
     s0 = devs.stream(d0, 0)
     pipelined(step, devs, 0, warmup)
@@ -405,7 +408,14 @@ def run_mode(step, devs, steps, warmup, dist):
         b.record(s0)
     devs.sync()
     iso = [a.elapsed_time(b) for a, b in ev]
-    stats = {"period_ms": period, "launch_alone_mean_ms": float(np.mean(iso)),
+    es0, es1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    es0.record(s0)
+    for _ in range(20):
+        step(0)
+    es1.record(s0)
+    devs.sync()
+    serial = es0.elapsed_time(es1) / 20
+    stats = {"period_ms": period, "launch_serial_ms": serial, "launch_alone_mean_ms": float(np.mean(iso)),
              "launch_alone_median_ms": float(np.median(iso)), "launch_alone_min_ms": float(np.min(iso)),
              "launch_alone_max_ms": float(np.max(iso))}
     if dist:
@@ -416,7 +426,8 @@ def run_mode(step, devs, steps, warmup, dist):
         allr = [None] * dist.get_world_size()
         dist.all_gather_object(allr, stats)
         stats = {"rank0": stats, "per_rank_period_ms": [r["period_ms"] for r in allr],
-                 "per_rank_launch_alone_ms": [r["launch_alone_mean_ms"] for r in allr]}
+                 "per_rank_launch_alone_ms": [r["launch_alone_mean_ms"] for r in allr],
+                 "per_rank_launch_serial_ms": [r["launch_serial_ms"] for r in allr]}
     return elapsed, period, stats
 
 
@@ -526,9 +537,14 @@ class Watchdog:
         self.t.cancel()
 
 
+def launch_ms(stats):
+    """Rank 0's mean launch duration (run_mode: 20 launches serialised on one stream, one event pair)."""
+    return (stats["rank0"] if "rank0" in stats else stats)["launch_serial_ms"]
+
+
 def shard_fields(gpus, F, n, el, km, stats, steps, bytes_per_frame):
     """Rate and roofline of one config's shards (rank 0's launch duration)."""
-    alone = (stats["rank0"] if "rank0" in stats else stats)["launch_alone_mean_ms"]
+    alone = launch_ms(stats)
     return {"value": gpus * F * steps / el, "unit": "frames/s", "ms_per_step": el / steps * 1e3,
             "kernel_ms": alone, "period_ms": km, "bytes_per_frame": bytes_per_frame,
             "roofline_frac": F * bytes_per_frame / (alone * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -651,7 +667,7 @@ def secondary(args, plan, frames, devs, n, F):
             p.extract_device(fr.data_ptr(), Fx, sets[k & 1][1], devs.stream(dev, k).cuda_stream)
         settle(st, devs, args.settle_ms)
         el, km, stats = run_mode(st, devs, args.steps, args.warmup, None)
-        alone = stats["launch_alone_mean_ms"]
+        alone = launch_ms(stats)
         return {"value": Fx * args.steps / el, "unit": "frames/s", "kernel_ms": alone, "period_ms": km,
                 "bytes_per_frame": bytes_per_frame,
                 "roofline_frac": Fx * bytes_per_frame / (alone * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -721,10 +737,10 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
     if use_gather:
         gather["vs_shards"] = gather["value"] / value_s
     elapsed = args.steps * 1e3 / (value / (gpus * F))  # ms for the K steps
-    # the roofline of the extraction kernel: its average launch duration, launches serialised on one
-    # stream with an event pair around each (what rocprofv3 --stats reports per dispatch); the
-    # launch period of the pipelined timed steps (value) is reported beside it
-    alone_ms = (stats_s["rank0"] if "rank0" in stats_s else stats_s)["launch_alone_mean_ms"]
+    # the roofline of the extraction kernel: its average launch duration, 20 launches serialised on
+    # one stream between one event pair (what rocprofv3 --stats reports per dispatch); the launch
+    # period of the pipelined timed steps (value) is reported beside it
+    alone_ms = launch_ms(stats_s)
     kernel_ms = alone_ms
     achieved = F * bytes_per_frame / (kernel_ms * 1e-3) / 1e9
     traffic, valu, traffic_note = extras.get("pmc") or (None, None, "not measured (--no-pmc or N > 1)")
@@ -776,9 +792,10 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                      "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
-                     "kernel_ms_source": "mean launch duration: 20 launches serialised on one stream after the "
-                                         "timed steps, an event pair around each (rocprofv3 --stats of "
-                                         "bench.py --single-stream: profiles/)",
+                     "kernel_ms_source": "mean launch duration: 20 launches back to back on one stream after "
+                                         "the timed steps, HIP events around them (step_event_ms.launch_serial_ms; "
+                                         "launch_alone_* = an event pair around each launch, which adds ~4 %); "
+                                         "rocprofv3 --stats of bench.py --single-stream: profiles/",
                      "period_ms": km_s,
                      "period_source": ("launch period of the timed steps: HIP events around the timed region / steps"
                                        + (" (one stream)" if args.single_stream else " (steps pipelined over two streams)")),

@@ -151,7 +151,7 @@ def test_bench_value_is_the_shards_rate():
 
     import bench
     args = types.SimpleNamespace(steps=10, warmup=2, precision="faithful", single_stream=False)
-    st = {"launch_alone_mean_ms": 0.6}
+    st = {"launch_alone_mean_ms": 0.6, "launch_serial_ms": 0.6}
     line = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, st,
                             {"status": "ok", "value": 2.8e9}, {})
     assert line["value"] == 3.5e9 and line["n_gpus"] == 8 and line["scaling"] == "weak"
@@ -170,7 +170,7 @@ def test_bench_c5_field_shape():
     import types
 
     import bench
-    st = {"launch_alone_mean_ms": 1.3}
+    st = {"launch_alone_mean_ms": 1.3, "launch_serial_ms": 1.3}
     one = bench.c5_field(1, 262144, 0.026, 1.3, st, 20, False)
     assert one["buffer_size"] == 2048 and one["frames_per_gpu"] == 262144 and one["frames_total"] == 262144
     assert one["bytes_per_frame"] == 4 * 2048 + 4 * 50 and one["features"] == bench.FEATURES
@@ -181,7 +181,7 @@ def test_bench_c5_field_shape():
     assert eight["frames_total"] == 2097152 and eight["gather"]["status"] == "not run"
     assert eight["kernel_ms"] == 1.3
     args = types.SimpleNamespace(steps=20, warmup=5, precision="faithful", single_stream=False)
-    line = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, {"launch_alone_mean_ms": 0.6},
+    line = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, {"launch_alone_mean_ms": 0.6, "launch_serial_ms": 0.6},
                             {"status": "ok", "value": 2.8e9}, {"c5": eight})
     assert line["value"] == 3.5e9 and line["c5"]["frames_total"] == 2097152
     p = bench.parse([])
@@ -196,13 +196,13 @@ def test_bench_line_carries_every_config():
 
     import bench
     args = types.SimpleNamespace(steps=20, warmup=5, precision="faithful", single_stream=False)
-    st = {"launch_alone_mean_ms": 0.6}
+    st = {"launch_alone_mean_ms": 0.6, "launch_serial_ms": 0.6}
     mf = {"instr_per_launch": 655360.0, "flop_per_launch": 512 * 655360.0, "busy_cycles_per_launch": 1.0,
           "gui_active_cycles": 1.0}
     valu = {"instr_per_frame": 1200.0, "cvt_per_frame": 400.0, "f64_per_frame": 450.0, "lds_per_frame": 97.0,
             "mfma_f64": dict(mf, flop_per_launch=512 * 458752.0), "mfma_f64_c4": dict(mf)}
     extras = {"pmc": (1.13e9, valu, "note"), "c2": {"value": 1e9}, "c3": {"value": 5e8}, "c4": {"value": 5e8, "kernel_ms": 0.5},
-              "c5": bench.c5_field(1, 262144, 0.026, 1.3, {"launch_alone_mean_ms": 1.3}, 20, False),
+              "c5": bench.c5_field(1, 262144, 0.026, 1.3, {"launch_alone_mean_ms": 1.3, "launch_serial_ms": 1.3}, 20, False),
               "mfcc_exact": {"value": 3.6e8, "kernel_ms": 0.75}, "latency": {"status": "ok", "c1": {"us_per_call": 25.0}}}
     line = bench.build_line(args, 1, "one", [], 262144, 1024, 4.5e8, 0.0116, 0.58, st, None, extras)
     assert line["value"] == 4.5e8 and "gather" not in line

@@ -28,7 +28,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 100 --warmup 20 --single-stream --no-cpu-baseline --no-host-path --no-pmc --no-every-output --no-fast --no-c2 --no-c3 --no-c4 --no-c5 --no-mfcc-exact --no-latency > $O/prof_bench.log 2>&1 || { tail -20 $O/prof_bench.log; exit 1; }
 tail -1 $O/prof_bench.log
 # the 100 timed (pipelined) launches' period, then the 20 single-stream launches after them
-python3 $R/tools/prof_summary.py $O/prof/run_kernel_trace.csv 100 "" 1 20 > $O/prof_summary.txt
+python3 $R/tools/prof_summary.py $O/prof/run_kernel_trace.csv 100 "" 1 40 > $O/prof_summary.txt
 step traffic
 $R/tools/gpu_traffic.sh > $O/traffic.log 2>&1 || { tail -20 $O/traffic.log; exit 1; }
 cp $R/gpurun_out/traffic/summary.json $O/pmc_traffic.json

@@ -6,7 +6,7 @@ bench is that many launches: mgx_extract_device's parts on two streams), the ste
 the matching kernel too: first start to last end of each group of `parts` dispatches, over
 the last k steps -- the figure the bench's per-step HIP events measure.
 With skip > 0 the last `skip` dispatches are left out first (bench.py's single-stream
-launches after its timed steps), and for extract kernels the launch period of the k
+launches after its timed steps: 20 with an event pair each, then 20 back to back, skip = 40), and for extract kernels the launch period of the k
 dispatches before them is printed: (last end - first start) / k -- what bench.py's events
 around its pipelined timed region measure (consecutive launches overlap by the drain).
 usage: prof_summary.py KERNEL_TRACE.csv [k] [name-substring] [parts] [skip]"""
@@ -31,6 +31,7 @@ def main():
     print("%-70s %6s %10s %10s %10s %10s" % ("kernel", "n", "mean_ms", "min_ms", "max_ms", "lastK_mean"))
     for name, v in sorted(by.items(), key=lambda kv: -sum(b - a for a, b in kv[1])):
         v.sort()
+        v_all = list(v)
         if skip and "extract_kernel" in name and len(v) > skip:
             alone = [(b - a) * 1e-6 for a, b in v[-skip:]]
             v = v[:-skip]
@@ -39,6 +40,12 @@ def main():
             print("  %s: launch period over the %d timed steps %.4f ms; the %d single-stream launches after "
                   "them: mean %.4f ms, median %.4f" % (name[:60], k, period, skip, sum(alone) / skip,
                                                         sorted(alone)[skip // 2]))
+            if skip >= 40:
+                # bench.py's last 20: back to back on one stream between one event pair (its kernel_ms)
+                ser = v_all[-20:]
+                print("  the last 20 (back to back, bench.py's launch_serial_ms): mean duration %.4f ms, "
+                      "(last end - first start) / 20 = %.4f ms" % (sum((b - a) for a, b in ser) * 1e-6 / 20,
+                                                                   (ser[-1][1] - ser[0][0]) * 1e-6 / 20))
         ts = [(b - a) * 1e-6 for a, b in v]  # ns -> ms
         kk = k * parts
         last = ts[-kk:]
