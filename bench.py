@@ -382,7 +382,7 @@ def run_mode(step, devs, steps, warmup, dist):
     launches), and one more of 20 launches back to back on one stream with one event pair around
     them all: the mean launch duration (plus the small dispatch gap between serialised launches),
     which is what rocprofv3 reports per dispatch -- an event pair around every launch adds its own
-    marker packets to each (~4 % of a 0.6 ms launch against the profiler's durations)."""
+    marker packets to each (~1 % of a 0.6 ms launch against the profiler's durations)."""
     d0 = devs.devs[0]
     s0 = devs.stream(d0, 0)
     pipelined(step, devs, 0, warmup)
@@ -794,7 +794,7 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
                      "kernel": "extract_kernel<%d>" % n, "kernel_ms": kernel_ms,
                      "kernel_ms_source": "mean launch duration: 20 launches back to back on one stream after "
                                          "the timed steps, HIP events around them (step_event_ms.launch_serial_ms; "
-                                         "launch_alone_* = an event pair around each launch, which adds ~4 %); "
+                                         "launch_alone_* = an event pair around each launch, which adds ~1 %); "
                                          "rocprofv3 --stats of bench.py --single-stream: profiles/",
                      "period_ms": km_s,
                      "period_source": ("launch period of the timed steps: HIP events around the timed region / steps"
