@@ -160,12 +160,13 @@ int mgx_plan_destroy(mgx_plan* plan);
 int mgx_plan_get_desc(const mgx_plan* plan, mgx_plan_desc* out_desc);
 
 /* Device-resident batch: frames and every non-NULL output are device pointers.
- * Asynchronous on `stream` (hipStream_t or NULL). A plan with MGX_FLAG_MFCC_REFERENCE
- * (and an MFCC output) also needs per-stream scratch: the power-row ring of its mel chains,
- * one per distinct stream the plan launches on (~2 KB x 8 per resident wave, tens of MB),
- * allocated on the first call on that stream (hipMalloc, which may synchronise the device:
- * make one untimed call per stream first, outside any stream capture) and kept until
- * mgx_plan_destroy. Plans without that flag allocate nothing here. */
+ * Asynchronous on `stream` (hipStream_t or NULL). The launch uses per-stream device scratch,
+ * one set per distinct stream the plan launches on: the scalar features' windows (5 KB per
+ * resident wave, ~20 MB) and, for a plan with MGX_FLAG_MFCC_REFERENCE and an MFCC output, the
+ * power-row ring of its mel chains (~2 KB x 8 per resident wave, tens of MB). A set is allocated
+ * on the first call on its stream (hipMalloc, which may synchronise the device: make one
+ * untimed call per stream first, outside any stream capture) and kept until mgx_plan_destroy,
+ * which waits for the launches that used it. */
 int mgx_extract_device(mgx_plan* plan, const float* frames, uint64_t num_frames,
                        const mgx_outputs* outputs, void* stream);
 

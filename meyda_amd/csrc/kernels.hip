@@ -702,6 +702,30 @@ struct FrameRec {
   float sharp_sum;
 };
 
+// A frame's inputs to the thirteen scalar formulas (scalar_value), as phase 2 leaves them in its
+// record: the first eight words and the last two of a FrameRec, copied word for word into the
+// wave's scalar window (scalar_pass).
+struct ScalIn {
+  double S[5];
+  double ln2sum;
+  double energy;
+  double band[1];  // the loudness total (FrameRec::band[0] after phase 2's loudness step)
+  int zcr;
+  int roll_m;
+  uint32_t loud_max;
+  float sharp_sum;
+};
+static_assert(sizeof(ScalIn) == 80, "10 words");
+static_assert(offsetof(FrameRec, band) == 56 && offsetof(FrameRec, zcr) == 504 && offsetof(FrameRec, sharp_sum) == 516,
+              "the scalar inputs: FrameRec words 0..7 and 63..64");
+#ifndef MGX_SCAL_DEFER
+#define MGX_SCAL_DEFER 1
+#endif
+// Scalars once per window of kScalBatches batches, one lane per frame (scalar_pass), instead of
+// one lane per (feature, frame) in every batch's phase 2 -- for launches that compute a spectrum
+// (KernelArgs::scal_defer; plan.cpp says when)
+constexpr bool kScalDefer = MGX_SCAL_DEFER;
+
 // Record fb (< 4) of the wave's batch and small per-lane offsets by 24-bit multiplies: the lane
 // indices come through opaque() (no range the compiler can see), and a 32-bit v_mul_lo_u32 /
 // 64-bit v_mad_u64_u32 is a multi-pass instruction where v_mul_u32_u24 is one VALU op.
@@ -1567,8 +1591,8 @@ __device__ __forceinline__ double rcp_d(double x) {
 // entries), formulas as written in the reference extractors. Every lane evaluates the shared
 // terms (moments, spread) and takes its feature's numerator and denominator (the loudness
 // quotients joined from a tail of their own: one reciprocal chain per batch instead of three).
-template <int N, bool SUB>
-__device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int sc) {
+template <int N, bool SUB, class Rec>
+__device__ __forceinline__ double scalar_value(KArgs* q, const Rec& rc, int sc) {
   constexpr int L = N / 2;
   const double S0 = rc.S[0];
   // utils.js:1-11 mu(p) = sum k^p a_k / sum a_k: one reciprocal and four products (S0 is
@@ -1626,6 +1650,43 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const FrameRec& rc, int
   }
   const double v = num * (k * rcp_d(den));
   return sc == MGX_RMS ? sqrt_d(v) : sc == MGX_PERCEPTUAL_SPREAD ? v * v : v;
+}
+
+// The scalar features of one window of a wave's batches (kScalDefer), one lane per frame: lane l
+// takes frame l & 3 of the window's batch l >> 2 (nbat batches; frame f0 + (l >> 2) fstep + (l & 3)),
+// its ScalIn from the wave's window in device memory (win: word c of lane l at c * 64 + l, phase 2
+// put it there), and stores every requested feature -- the formulas of scalar_value, evaluated
+// with each feature a constant, so the thirteen share their common terms and nothing diverges.
+template <int N, bool SUB, class WinPtr>
+__device__ __forceinline__ void scalar_pass(KArgs* q, WinPtr win, void* const* kptr, uint64_t f0, uint64_t fstep, int nbat,
+                                            int lane) {
+  // the window's words were stored by this wave (phase 2 of each batch): visible to its loads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const auto w = win + (unsigned)lane;
+  uint64_t wd[10];
+#pragma unroll
+  for (int c = 0; c < 10; ++c) wd[c] = w[c * 64];
+  ScalIn r;
+  __builtin_memcpy(&r, wd, sizeof(r));
+  const uint64_t f = f0 + (uint64_t)(lane >> 2) * fstep + (uint64_t)(lane & 3);
+  const bool ok = (lane >> 2) < nbat && f < q->num_frames;
+  double v[MGX_NUM_SCALARS];
+#pragma unroll
+  for (int sc = 0; sc < MGX_NUM_SCALARS; ++sc) v[sc] = scalar_value<N, SUB>(q, r, sc);
+  const bool f64 = q->scalar_f64;
+#pragma unroll
+  for (int sc = 0; sc < MGX_NUM_SCALARS; ++sc) {
+    // the output pointers from the workgroup's constant table, as wave-uniform values
+    const uint64_t pv = reinterpret_cast<const uint64_t*>(kptr)[sc];
+    const uint64_t pu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pv) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pv >> 32)) << 32;
+    if (pu == 0) continue;
+    if (ok) {
+      if (f64) gbl(reinterpret_cast<double*>(pu))[f] = v[sc];
+      else gbl(reinterpret_cast<float*>(pu))[f] = (float)v[sc];
+    }
+  }
 }
 
 // mfcc.js:64: Math.log of the batch's band energies (lm[lmo + band] of its FPW records), stored
@@ -1973,9 +2034,23 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         if (CHAIN && q->chain_pair) mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 32, f0 - wstride * FPW);  // the pair's first batch
       }
       MGX_MARK(dct_done);
+      const bool defer = kScalDefer && q->scal_defer;
+      if (defer) {
+        // the batch's scalar inputs into the wave's window (10 words per frame, lanes 0..39: frame
+        // l2 / 10, word l2 % 10), the scalars of the window once it is full (scalar_pass)
+        const auto win = uniform_ptr(gbl(q->scal_rows) + ((uint64_t)blockIdx.x * 4 + wave) * (uint64_t)kScalWords);
+        const int slot = it & (kScalBatches - 1);
+        if (l2 < 10 * FPW) {
+          const int fb = (int)(__umul24((unsigned)l2, 205u) >> 11);  // l2 / 10 for l2 < 40
+          const int c = l2 - 10 * fb;
+          const unsigned off = 8u * (unsigned)c + (c >= 8 ? 440u : 0u);  // words 0..7, then 63..64
+          const uint64_t wv = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const unsigned char*>(&rec_at(recs, fb)) + off);
+          win[__umul24((unsigned)c, 64u) + (unsigned)(4 * slot + fb)] = wv;
+        }
+      }
       // the scalar features: one lane per (feature, frame); the loudness total, perceptual
       // spread and sharpness from the loudness step's record entries (16 x 4 lanes at most)
-      for (int i = l2; i < (MGX_PERCEPTUAL_SHARPNESS + 1) * FPW; i += 64) {
+      for (int i = l2; !defer && i < (MGX_PERCEPTUAL_SHARPNESS + 1) * FPW; i += 64) {
         const int sc = (int)((unsigned)i / FPW), fb = i & (FPW - 1);
         const uint64_t f = f0 + fb;
         void* dst = reinterpret_cast<void* const*>(smem + LY::kc_off)[sc];
@@ -1998,6 +2073,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       const uint64_t g = (b - wave) / 4;
       if (g * 4 + 3 < nb && g % G::GROUP_SYNC == G::GROUP_SYNC - 1) __builtin_amdgcn_s_barrier();
     }
+    // A full scalar window: its pass right after the group barrier (a window ends on an odd group,
+    // where the barrier is), so the workgroup's four waves write their 16-byte pieces of each
+    // scalar output line together and the L2 merges them, as the per-batch form's writes.
+    if (kScalDefer && (it & (kScalBatches - 1)) == kScalBatches - 1) {
+      KArgs* q = args_ptr();
+      if (q->scal_defer) {
+        prio_hi<4>();
+        scalar_pass<N, SUB>(q, uniform_ptr(gbl(q->scal_rows) + ((uint64_t)blockIdx.x * 4 + wave) * (uint64_t)kScalWords),
+                            reinterpret_cast<void* const*>(smem + LY::kc_off),
+                            (b - (uint64_t)(kScalBatches - 1) * wstride) * FPW, wstride * FPW, kScalBatches, opaque(lane));
+        prio_lo<4>();
+      }
+    }
+  }
+  if (kScalDefer && args_ptr()->scal_defer && (it & (kScalBatches - 1)) != 0) {
+    // the wave's last window, with fewer than kScalBatches batches
+    KArgs* q = args_ptr();
+    const int nbat = it & (kScalBatches - 1), l2 = opaque(lane);
+    prio_hi<4>();
+    scalar_pass<N, SUB>(q, uniform_ptr(gbl(q->scal_rows) + ((uint64_t)blockIdx.x * 4 + wave) * (uint64_t)kScalWords),
+                        reinterpret_cast<void* const*>(smem + LY::kc_off), (b0 + (uint64_t)(it - nbat) * wstride) * FPW,
+                        wstride * FPW, nbat, l2);
+    prio_lo<4>();
   }
   if constexpr (CHAIN) {
     // paired batches: a wave whose last batch opened a pair finishes that batch's mfcc alone

@@ -8,6 +8,12 @@
 namespace mgx {
 
 constexpr int kMaxMel = 64;
+// The scalar features run once per window of kScalBatches batches of a wave (kernels.hip
+// scalar_pass), one lane per frame: the window's per-frame inputs (10 8-byte words each, the
+// record's S[0..4], ln2sum, energy, loudness total, zcr | roll_m, loud_max | sharp_sum) wait in
+// device memory, kScalWords words per wave.
+constexpr int kScalBatches = 16;
+constexpr int kScalWords = 10 * 4 * kScalBatches;
 constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
@@ -62,11 +68,13 @@ struct KernelArgs {
   int need_prefix;       // rolloff or loudness: the prefix row (rolloff count, bark band sums)
   int need_energy;       // rms or energy: the wave sum of the squares (SUB kernel)
   int need_zcr;          // zcr: the sign-change ballots (SUB kernel)
+  int scal_defer;        // the scalars by windows (scalar_pass): a spectrum is computed and a scalar requested
   int dct_sequential;    // MGX_FLAG_DCT_SEQUENTIAL: the DCT as VALU FMAs in the reference's order
   int wg_ranks;          // workgroups per CU when the grid is the resident one (else 1): their work shares
   int chain_groups;      // 8-step groups of the mel chain tracks (0: the segmented scan)
   int chain_pair;        // the chains of two consecutive batches of a wave run together (8 frames, nfilt <= 31)
   float* chain_rows;     // the chains' power rows: 2 FPW x N/2 floats per wave of the grid (kernels.hip mel_chains)
+  uint64_t* scal_rows;   // the scalar window: kScalWords 8-byte words per wave of the grid (kernels.hip scalar_pass)
 };
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.

@@ -450,13 +450,15 @@ struct mgx_plan {
   int cus = 0;  // compute units of the plan's device
   int chain_groups = 0;  // MGX_FLAG_MFCC_REFERENCE: 8-step groups of the mel chains (chain_schedule)
   int chain_pair = 0;  // ... over two consecutive batches of a wave (8 frames)
-  // the mel chains' power-row rings (kernels.hip KGeo::GROWS), one per stream a launch used: the
-  // launches of one stream run in order, those of two streams may overlap. Each ring's event is
+  // Per-stream device scratch, one set per stream a launch used (the launches of one stream run
+  // in order, those of two streams may overlap): the scalar windows (kernels.hip scalar_pass) and,
+  // for the reference-order MFCC, the mel chains' power rows (mel_chains). Each set's event is
   // recorded after every launch that uses it, so destroy waits for exactly those launches (the
   // stream itself may be gone by then).
   struct ChainRing {
     void* stream;
-    float* rows;
+    uint64_t* scal;
+    float* rows;  // null until a reference-order MFCC launch on the stream
     hipEvent_t done;
   };
   std::vector<ChainRing> chain_rings;
@@ -659,7 +661,8 @@ int mgx_plan_destroy(mgx_plan* p) {
   for (auto& r : p->chain_rings) {
     (void)hipEventSynchronize(r.done);
     (void)hipEventDestroy(r.done);
-    (void)hipFree(r.rows);
+    (void)hipFree(r.scal);
+    if (r.rows) (void)hipFree(r.rows);
   }
   if (p->s_copy) (void)hipStreamSynchronize(p->s_copy);
   if (p->s_comp) (void)hipStreamSynchronize(p->s_comp);
@@ -720,33 +723,50 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   a.need_prefix = a.need_loudness || o->scalars[MGX_SPECTRAL_ROLLOFF];
   a.need_energy = o->scalars[MGX_RMS] || o->scalars[MGX_ENERGY];
   a.need_zcr = o->scalars[MGX_ZCR] != nullptr;
+  bool any_scalar = false;
+  for (int i = 0; i < MGX_NUM_SCALARS; ++i) any_scalar = any_scalar || o->scalars[i];
   const uint64_t fb = (uint64_t)mgx::frames_per_batch(p->n);
   const uint64_t nb = (nframes + fb - 1) / fb;
   const int grid = (int)std::min<uint64_t>(nb, (uint64_t)p->grid_cap);
   a.wg_ranks = grid == p->grid_cap && p->cus > 0 ? p->grid_cap / p->cus : 1;
+  // The scalars run once per window of a wave's batches (kernels.hip scalar_pass) when the launch
+  // computes a spectrum (VALU-bound there: 0.7-1.9 % faster by N, outputs identical) and its waves
+  // get at least 8 batches each on average. A time-only launch is HBM-bound, and the windows' late,
+  // per-wave output writes lost it 18 %; with a few batches per wave (C2's 65,536 frames: 3) the
+  // one pass at the end of each wave lengthens the launch's tail (+1.6 %). Those, and launches
+  // without a scalar output, keep the per-batch form.
+  a.scal_defer = a.need_spectrum && any_scalar && nb >= (uint64_t)grid * 8;
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  hipEvent_t ring_done = nullptr;
-  if (a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) {
-    for (auto& r : p->chain_rings)
-      if (r.stream == stream) {
-        a.chain_rows = r.rows;
-        ring_done = r.done;
-      }
-    if (!a.chain_rows) {
-      // 2 FPW x N/2 floats for each wave of the largest grid (4 waves per workgroup); the first
-      // launch on a stream allocates its ring (include/meyda_gpu.h)
-      const size_t bytes = (size_t)p->grid_cap * 4 * 2 * (size_t)(fb / 4) * (size_t)p->L * sizeof(float);
-      e = hipMalloc(reinterpret_cast<void**>(&a.chain_rows), bytes);
-      if (e != hipSuccess) return hip_fail(e, "hipMalloc(mel chain rows)");
-      e = hipEventCreateWithFlags(&ring_done, hipEventDisableTiming);
-      if (e != hipSuccess) {
-        (void)hipFree(a.chain_rows);
-        return hip_fail(e, "hipEventCreate(mel chain rows)");
-      }
-      p->chain_rings.push_back({stream, a.chain_rows, ring_done});
+  // the stream's scratch set (the first launch on a stream allocates it, include/meyda_gpu.h)
+  mgx_plan::ChainRing* ring = nullptr;
+  for (auto& r : p->chain_rings)
+    if (r.stream == stream) ring = &r;
+  if (!ring) {
+    // kScalWords words for each wave of the largest grid (4 waves per workgroup)
+    uint64_t* scal = nullptr;
+    e = hipMalloc(reinterpret_cast<void**>(&scal), (size_t)p->grid_cap * 4 * mgx::kScalWords * sizeof(uint64_t));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(scalar windows)");
+    hipEvent_t done = nullptr;
+    e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      (void)hipFree(scal);
+      return hip_fail(e, "hipEventCreate(stream scratch)");
     }
+    p->chain_rings.push_back({stream, scal, nullptr, done});
+    ring = &p->chain_rings.back();
   }
+  a.scal_rows = ring->scal;
+  if (a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) {
+    if (!ring->rows) {
+      // 2 FPW x N/2 floats for each wave of the largest grid (4 waves per workgroup)
+      const size_t bytes = (size_t)p->grid_cap * 4 * 2 * (size_t)(fb / 4) * (size_t)p->L * sizeof(float);
+      e = hipMalloc(reinterpret_cast<void**>(&ring->rows), bytes);
+      if (e != hipSuccess) return hip_fail(e, "hipMalloc(mel chain rows)");
+    }
+    a.chain_rows = ring->rows;
+  }
+  hipEvent_t ring_done = ring->done;
   e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "extract kernel launch");
   if (ring_done) {

@@ -311,3 +311,40 @@ def test_small_host_batches_equal_staged_path(capi, n):
         a2, b2 = small.extract(y, feats), staged.extract(y, feats)
         for k in a2:
             assert np.array_equal(a2[k].view(np.uint8), b2[k].view(np.uint8)), (F, k, "second call")
+
+
+C3_SET = ["spectralCentroid", "spectralFlatness", "spectralSlope", "spectralRolloff", "spectralSpread",
+          "spectralSkewness", "spectralKurtosis", "loudness", "perceptualSpread", "perceptualSharpness"]
+
+
+@pytest.mark.parametrize("n", [256, 512, 1024, 2048])
+def test_scalar_windows_equal_per_batch_form(capi, n):
+    """A launch whose waves get 8 or more batches each computes the scalar features once per
+    window of 16 batches, one lane per frame (kernels.hip scalar_pass); a smaller launch computes
+    them per batch, one lane per (feature, frame). The same frames through both must give the same
+    bits: a ragged 262,157-frame launch (partial batch, partial last windows) against chunks of
+    16,384 frames, every feature, C3's subset, float32 and float64 scalars, the reference-order MFCC,
+    and non-finite, silent and loud frames among them (a NaN output may differ in its sign bit:
+    the formulas are the same, the instructions that propagate the NaN are not)."""
+    import torch
+    F, chunk = 262144 + 13, 16384
+    x = torch.empty(F, n, dtype=torch.float32, device="cuda")
+    capi.synth_frames_device(x, 0x5CA1AB1E)
+    x[5, 3] = float("nan")
+    x[70000, :] = 0.0
+    x[140001, 9] = float("inf")
+    x[200003, :] *= 1e19
+    x[F - 1, 0] = float("-inf")
+    for kw, feats in (({"scalar_f64": True}, capi.ALL_FEATURES), ({}, capi.ALL_FEATURES), ({}, C3_SET),
+                      ({"scalar_f64": True, "mfcc_reference": True}, capi.ALL_FEATURES)):
+        plan = capi.Plan(buffer_size=n, **kw)
+        whole = plan.extract_torch(x, feats)
+        parts = [plan.extract_torch(x[i:i + chunk].contiguous(), feats) for i in range(0, F, chunk)]
+        torch.cuda.synchronize()
+        for k, v in whole.items():
+            w = torch.cat([p[k] for p in parts])
+            # bit for bit, except that a NaN may differ in sign (the reference's NaN has none)
+            nan = torch.isnan(v)
+            assert torch.equal(nan, torch.isnan(w)), (n, kw, k)
+            assert torch.equal(v[~nan].view(torch.uint8), w[~nan].view(torch.uint8)), (n, kw, k)
+        plan.close()
