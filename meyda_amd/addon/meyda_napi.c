@@ -243,6 +243,11 @@ typedef struct {
   uint64_t pcm_frames;
   uint32_t pcm_format, pcm_channels, pcm_channel;
   mgx_outputs out;
+  /* The outputs are written straight into JS ArrayBuffers (napi_create_arraybuffer), held by
+   * references until the result object takes them. (External ArrayBuffers over malloc'd memory
+   * with a free finalizer made Node 12 abort at exit: v8impl ArrayBufferReference::Finalize's
+   * assertion during the environment's teardown.) */
+  napi_ref refs[NSLOTS];
   void* bufs[NSLOTS];
   size_t bytes[NSLOTS];
   int want[NSLOTS];
@@ -254,8 +259,13 @@ typedef struct {
   char err[512];
 } job;
 
-static void job_free_buffers(job* j) {
-  for (int i = 0; i < NSLOTS; ++i) free(j->bufs[i]);
+static void job_free_buffers(napi_env env, job* j) {
+  for (int i = 0; i < NSLOTS; ++i)
+    if (j->refs[i]) {
+      napi_delete_reference(env, j->refs[i]);
+      j->refs[i] = NULL;
+      j->bufs[i] = NULL;
+    }
 }
 
 /* Parse the features argument (string or array of strings) into wanted output slots. */
@@ -338,11 +348,13 @@ static int job_alloc(napi_env env, job* j, napi_value feats) {
     else if (i == SLOT_AMP || i == SLOT_POW) b = F * L * 4;
     else b = F * n * 4;
     j->bytes[i] = b;
-    j->bufs[i] = malloc(b ? b : 1);
-    if (!j->bufs[i]) {
+    napi_value abv;
+    void* data = NULL;
+    if (napi_create_arraybuffer(env, b, &data, &abv) != napi_ok || napi_create_reference(env, abv, 1, &j->refs[i]) != napi_ok) {
       napi_throw_error(env, NULL, "out of host memory");
       return 0;
     }
+    j->bufs[i] = data;
   }
   for (int i = 0; i < MGX_NUM_SCALARS; ++i) j->out.scalars[i] = j->bufs[i];
   j->out.loudness_specific = (float*)j->bufs[SLOT_LOUD];
@@ -434,16 +446,9 @@ static void job_run(job* j) {
   if (j->rc) snprintf(j->err, sizeof j->err, "%s", mgx_last_error());
 }
 
-static void free_ab(napi_env env, void* data, void* hint) {
-  (void)env;
-  (void)hint;
-  free(data);
-}
-
 static napi_value typed(napi_env env, job* j, int slot, napi_typedarray_type t, size_t elem) {
   napi_value ab, ta;
-  if (napi_create_external_arraybuffer(env, j->bufs[slot], j->bytes[slot], free_ab, NULL, &ab) != napi_ok) return NULL;
-  j->bufs[slot] = NULL; /* ownership moved to the ArrayBuffer */
+  if (napi_get_reference_value(env, j->refs[slot], &ab) != napi_ok) return NULL;
   if (napi_create_typedarray(env, t, j->bytes[slot] / elem, ab, 0, &ta) != napi_ok) return NULL;
   return ta;
 }
@@ -485,19 +490,19 @@ static napi_value extract_common(napi_env env, napi_callback_info info, int wav)
   }
   if (!(wav ? job_prepare_wav(env, &j, argv[1], argv[2], argc > 3 ? argv[3] : NULL)
             : job_prepare(env, &j, argv[1], argv[2]))) {
-    job_free_buffers(&j);
+    job_free_buffers(env, &j);
     return NULL;
   }
   job_run(&j);
   if (j.rc) {
-    job_free_buffers(&j);
+    job_free_buffers(env, &j);
     char code[16];
     snprintf(code, sizeof code, "%d", j.rc);
     napi_throw_error(env, code, j.err);
     return NULL;
   }
   napi_value r = job_result(env, &j);
-  job_free_buffers(&j);
+  job_free_buffers(env, &j);
   return r;
 }
 
@@ -524,7 +529,7 @@ static void async_complete(napi_env env, napi_status status, void* data) {
   napi_delete_reference(env, j->frames_ref);
   napi_delete_reference(env, j->plan_ref);
   napi_delete_async_work(env, j->work);
-  job_free_buffers(j);
+  job_free_buffers(env, j);
   free(j);
   if (box->finalized) plan_box_free(box);
 }
@@ -548,7 +553,7 @@ static napi_value extract_async_common(napi_env env, napi_callback_info info, in
   }
   if (!(wav ? job_prepare_wav(env, j, argv[1], argv[2], argc > 3 ? argv[3] : NULL)
             : job_prepare(env, j, argv[1], argv[2]))) {
-    job_free_buffers(j);
+    job_free_buffers(env, j);
     free(j);
     return NULL;
   }

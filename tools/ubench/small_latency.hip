@@ -3,7 +3,8 @@
 //   A  hipStreamSynchronize (what extract_host_small does),
 //   B  a host spin on the mapped output words (sentinel bits -> value), then the stream sync,
 //   C  an empty kernel + hipStreamSynchronize (the launch and wake-up floor),
-//   D  the kernel's own duration between two events.
+//   E  a busy loop on hipStreamQuery, F  an event and a busy loop on hipEventQuery,
+//   D  the kernel's own duration between two events, G  the same on device-resident frames and outputs.
 // Build: hipcc --offload-arch=gfx950 -O2 -I include -o tools/ubench/small_latency tools/ubench/small_latency.hip \
 //          -L meyda_amd -lmeyda_gpu -Wl,-rpath,$PWD/meyda_amd
 // usage: small_latency [N] [calls]
@@ -66,10 +67,20 @@ int main(int argc, char** argv) {
   volatile uint32_t* w0 = reinterpret_cast<volatile uint32_t*>(hout);
   volatile uint32_t* w1 = reinterpret_cast<volatile uint32_t*>(hout + 16);
   const uint32_t kSentinel = 0xFFBADBADu;  // a NaN payload the kernel never writes for finite input
+  // G: the same kernel on device-resident frames and outputs (no PCIe in the kernel's chain)
+  float *gin, *gout;
+  CK(hipMalloc((void**)&gin, n * sizeof(float)));
+  CK(hipMalloc((void**)&gout, 256));
+  CK(hipMemcpy(gin, hin, n * sizeof(float), hipMemcpyHostToDevice));
+  mgx_outputs og;
+  memset(&og, 0, sizeof(og));
+  og.scalars[MGX_RMS] = gout;
+  og.scalars[MGX_SPECTRAL_CENTROID] = gout + 16;
+  std::vector<double> tg;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  std::vector<double> ta, tb, tc, td, tl;
+  std::vector<double> ta, tb, tc, td, tl, te, tf;
   for (int it = 0; it < calls + 50; ++it) {
     // A: launch + stream synchronise
     double t0 = now_us();
@@ -86,6 +97,19 @@ int main(int argc, char** argv) {
     }
     double t4 = now_us();
     CK(hipStreamSynchronize(s));
+    // E: launch + a busy loop on hipStreamQuery
+    double t7 = now_us();
+    if (mgx_extract_device(p, din, 1, &o, s) != MGX_OK) return 1;
+    while (hipStreamQuery(s) == hipErrorNotReady) {
+    }
+    double t8 = now_us();
+    // F: launch + event record + a busy loop on hipEventQuery
+    double t9 = now_us();
+    if (mgx_extract_device(p, din, 1, &o, s) != MGX_OK) return 1;
+    CK(hipEventRecord(e1, s));
+    while (hipEventQuery(e1) == hipErrorNotReady) {
+    }
+    double t10 = now_us();
     // C: empty kernel
     double t5 = now_us();
     empty_kernel<<<1, 64, 0, s>>>();
@@ -98,17 +122,29 @@ int main(int argc, char** argv) {
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipEventRecord(e0, s));
+    if (mgx_extract_device(p, gin, 1, &og, s) != MGX_OK) return 1;
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float msg = 0;
+    CK(hipEventElapsedTime(&msg, e0, e1));
     if (it >= 50) {
+      tg.push_back(msg * 1e3);
       ta.push_back(t2 - t0);
       tl.push_back(t1 - t0);
       tb.push_back(t4 - t3);
       tc.push_back(t6 - t5);
       td.push_back(ms * 1e3);
+      te.push_back(t8 - t7);
+      tf.push_back(t10 - t9);
     }
   }
   printf("{\"n\": %d, \"calls\": %d, \"launch_sync_us\": %.2f, \"launch_call_us\": %.2f, \"launch_spin_us\": %.2f, "
-         "\"empty_kernel_sync_us\": %.2f, \"kernel_event_us\": %.2f, \"rms\": %.9g, \"centroid\": %.9g}\n",
-         n, calls, median(ta), median(tl), median(tb), median(tc), median(td), hout[0], hout[16]);
+         "\"launch_stream_query_us\": %.2f, \"launch_event_query_us\": %.2f, "
+         "\"empty_kernel_sync_us\": %.2f, \"kernel_event_us\": %.2f, \"kernel_event_device_io_us\": %.2f, "
+         "\"rms\": %.9g, \"centroid\": %.9g}\n",
+         n, calls, median(ta), median(tl), median(tb), median(te), median(tf), median(tc), median(td), median(tg), hout[0],
+         hout[16]);
   mgx_plan_destroy(p);
   return 0;
 }
