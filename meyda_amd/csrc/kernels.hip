@@ -1934,6 +1934,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     // ------------------------------------------------------------- phase 1
     for (int j = 0; j < FPW; ++j) {
       const uint64_t f = f0 + j;
+      // the last batch's frames past the end: nothing to compute (phase 2 stores nothing for them).
+      // A launch of 1-3 frames would otherwise run 4 frames in its one wave (the real-time path's
+      // one-frame launch: ~4x its serial time).
+      if (f >= nf) break;
       float x[CH];
       GF next = nullptr;
       if constexpr (G::PF == 1) {
