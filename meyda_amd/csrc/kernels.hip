@@ -1776,6 +1776,22 @@ __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
   }
 }
 
+// The completion word of a small host batch (KernelArgs::done_flag): this wave's output stores
+// complete and visible to the host (a system-scope release), then one count per wave from lane 0
+// (a vector atomic); the wave that makes the count whole resets it for the next launch and
+// releases done_seq to the host word. The host, polling that word, reads the outputs without
+// waiting for the kernel's completion to reach the runtime (profiles/r04_small_latency.txt).
+__device__ __forceinline__ void done_signal(KArgs* q, int lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (lane == 0) {
+    const uint32_t before = __hip_atomic_fetch_add(q->done_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (before + 1 == q->done_waves) {
+      __hip_atomic_store(q->done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(q->done_flag, q->done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 #if MGX_WAVE_TIMES
 // (diagnostic build only, tools/wave_times.py) per wave: start, after the prologue, end (the
 // 100 MHz real-time clock) and the CU id / workgroup
@@ -2117,6 +2133,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       prio_lo<4>();
     }
   }
+  if (args_ptr()->done_flag) done_signal(args_ptr(), opaque(lane));
 #if MGX_WAVE_TIMES
   if (lane == 0 && blockIdx.x < 16384) {
     auto g = (__attribute__((address_space(1))) unsigned long long*)g_wave_times + ((uint64_t)blockIdx.x * 4 + wave) * 4;

@@ -69,6 +69,13 @@ struct KernelArgs {
   int need_energy;       // rms or energy: the wave sum of the squares (SUB kernel)
   int need_zcr;          // zcr: the sign-change ballots (SUB kernel)
   int scal_defer;        // the scalars by windows (scalar_pass): a spectrum is computed and a scalar requested
+  // Small host batches (plan.cpp extract_host_small): every wave counts itself in done_count at
+  // its end, after its output stores are visible to the host, and the last one sets the mapped
+  // host word done_flag to done_seq, which the host polls instead of synchronising the stream.
+  uint32_t* done_flag;   // null: no completion word
+  uint32_t* done_count;  // device memory, 0 between launches (the last wave resets it)
+  uint32_t done_seq;
+  uint32_t done_waves;   // waves in the grid
   int dct_sequential;    // MGX_FLAG_DCT_SEQUENTIAL: the DCT as VALU FMAs in the reference's order
   int wg_ranks;          // workgroups per CU when the grid is the resident one (else 1): their work shares
   int chain_groups;      // 8-step groups of the mel chain tracks (0: the segmented scan)

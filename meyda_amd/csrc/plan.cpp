@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -473,10 +474,20 @@ struct mgx_plan {
   hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr}, ev_back[2] = {nullptr, nullptr};
   // small host batches (kSmallBatchFrames): pinned, device-mapped, coherent host buffers
   uint64_t small_max = kSmallBatchFrames;
+  // the small path's completion word (KernelArgs::done_flag): a mapped host word, the device
+  // counter of finished waves and the launch sequence number
+  uint32_t* h_done = nullptr;
+  uint32_t* d_done_count = nullptr;
+  uint32_t done_seq = 0;
   float* h_in = nullptr;
   unsigned char* h_out = nullptr;
   size_t h_in_bytes = 0, h_out_bytes = 0;
 };
+
+namespace {
+int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o, void* stream,
+                        const uint32_t* done);
+}  // namespace
 
 extern "C" {
 
@@ -677,6 +688,8 @@ int mgx_plan_destroy(mgx_plan* p) {
   if (p->s_comp) (void)hipStreamDestroy(p->s_comp);
   if (p->h_in) (void)hipHostFree(p->h_in);
   if (p->h_out) (void)hipHostFree(p->h_out);
+  if (p->h_done) (void)hipHostFree(p->h_done);
+  if (p->d_done_count) (void)hipFree(p->d_done_count);
   delete p;
   return MGX_OK;
 }
@@ -688,6 +701,16 @@ int mgx_plan_get_desc(const mgx_plan* p, mgx_plan_desc* out) {
 }
 
 int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o, void* stream) {
+  return extract_device_impl(p, frames, nframes, o, stream, nullptr);
+}
+
+}  // extern "C"
+
+namespace {
+
+// mgx_extract_device, and with `done` (the small host path) the launch's completion word
+int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o, void* stream,
+                        const uint32_t* done) {
   if (!p || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL plan or outputs");
   if (nframes == 0) return MGX_OK;
   if (!frames) return fail(MGX_E_INVALID_ARGUMENT, "frames is NULL");
@@ -767,6 +790,12 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
     a.chain_rows = ring->rows;
   }
   hipEvent_t ring_done = ring->done;
+  if (done) {
+    a.done_flag = const_cast<uint32_t*>(done);
+    a.done_count = p->d_done_count;
+    a.done_seq = p->done_seq;
+    a.done_waves = (uint32_t)grid * 4;
+  }
   e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "extract kernel launch");
   if (ring_done) {
@@ -776,7 +805,7 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
   return MGX_OK;
 }
 
-}  // extern "C"
+}  // namespace
 
 namespace {
 
@@ -901,13 +930,49 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
     both(o->complex_imag, at[18], d.complex_imag, r.complex_imag);
     return r;
   }();
-  rc = mgx_extract_device(p, static_cast<const float*>(din), nframes, &d, p->s_comp);
+  if (!p->h_done) {
+    uint32_t* hd = nullptr;
+    e = hipHostMalloc(reinterpret_cast<void**>(&hd), 64, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(completion word)");
+    *hd = 0;
+    e = hipMalloc(reinterpret_cast<void**>(&p->d_done_count), sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(p->d_done_count, 0, sizeof(uint32_t));
+    if (e != hipSuccess) {
+      (void)hipHostFree(hd);
+      return hip_fail(e, "completion counter");
+    }
+    p->h_done = hd;
+  }
+  uint32_t* ddone = nullptr;
+  e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ddone), p->h_done, 0);
+  if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer(completion word)");
+  p->done_seq = p->done_seq + 1 ? p->done_seq + 1 : 1;  // never 0, the word's initial value
+  rc = extract_device_impl(p, static_cast<const float*>(din), nframes, &d, p->s_comp, ddone);
   if (rc) {
     (void)hipStreamSynchronize(p->s_comp);
     return rc;
   }
-  e = hipStreamSynchronize(p->s_comp);
-  if (e != hipSuccess) return hip_fail(e, "small host batch");
+  // The last wave of the launch releases done_seq to the host word after every output store is
+  // visible (kernels.hip done_signal): polling it returns ~9 us sooner than waiting for the
+  // stream (tools/ubench/small_latency.hip). Past 20 ms (a busy device) the wait blocks on the
+  // stream instead, which also reports a failed launch.
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    bool seen = false;
+    for (unsigned spins = 0;; ++spins) {
+      if (__atomic_load_n(p->h_done, __ATOMIC_ACQUIRE) == p->done_seq) {
+        seen = true;
+        break;
+      }
+      if ((spins & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+    }
+    if (!seen) {
+      e = hipStreamSynchronize(p->s_comp);
+      if (e != hipSuccess) return hip_fail(e, "small host batch");
+      if (__atomic_load_n(p->h_done, __ATOMIC_ACQUIRE) != p->done_seq)
+        return fail(MGX_E_DEVICE, "small host batch: the launch completed without its completion word");
+    }
+  }
   for (int k = 0; k < MGX_NUM_SCALARS; ++k)
     if (o->scalars[k]) memcpy(o->scalars[k], h.scalars[k], nframes * ss);
   if (o->loudness_specific) memcpy(o->loudness_specific, h.loudness_specific, nframes * nb * 4);
