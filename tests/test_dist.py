@@ -129,9 +129,11 @@ def _worker(rank, world, port, total, n, nch, q):
         q.put(("error: %r" % (e,), rank))
 
 
-@pytest.mark.parametrize("total,nch", [(64, 1), (67, 3), (40, 8)])  # even and ragged shards, chunk counts
-def test_gather_protocol_world2_matches_single_process(total, nch):
-    world, n = 2, 512
+# even and ragged shards, chunk counts; 4 ranks rehearse a wider gather (every peer into rank 0), and
+# N = 2048 is C5's frame size
+@pytest.mark.parametrize("world,n,total,nch", [(2, 512, 64, 1), (2, 512, 67, 3), (2, 512, 40, 8), (4, 512, 131, 3),
+                                               (4, 2048, 37, 8)])
+def test_gather_protocol_matches_single_process(world, n, total, nch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
@@ -141,7 +143,7 @@ def test_gather_protocol_world2_matches_single_process(total, nch):
     res = [q.get(timeout=240) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
-    assert sorted(res, key=lambda t: t[1]) == [("ok", 0), ("ok", 1)], res
+    assert sorted(res, key=lambda t: t[1]) == [("ok", r) for r in range(world)], res
 
 
 def test_bench_value_is_the_shards_rate():
