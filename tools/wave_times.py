@@ -4,7 +4,7 @@ every wave's start, end of prologue and end on the 100 MHz real-time clock plus 
 the last of a run of back-to-back launches on one stream (the persistent grid, or an
 over-subscribed one with MGX_GRID_CAP). Prints the start ramp, the prologue, the finishing
 spread (the drain) and the mean end per XCD, relative to the launch.
-usage: wave_times.py LIB [--n N] [--frames F]"""
+usage: wave_times.py LIB [--n N] [--frames F] [--features a,b,...]"""
 import argparse
 import ctypes
 import os
@@ -23,12 +23,14 @@ def main():
     ap.add_argument("lib")
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--frames", type=int, default=262144)
+    ap.add_argument("--features", default="all", help="comma-separated feature names (default every per-frame feature)")
     a = ap.parse_args()
     n, F = a.n, a.frames
     x = torch.empty(F, n, dtype=torch.float32, device="cuda")
     capi.synth_frames_device(x, 0x6D657964)
     plan0 = capi.Plan(buffer_size=n)
-    _, o = plan0.alloc_outputs(F, capi.ALL_FEATURES)
+    feats = capi.ALL_FEATURES if a.features == "all" else a.features.split(",")
+    _, o = plan0.alloc_outputs(F, feats)
     L = ctypes.CDLL(a.lib)
     L.mgx_plan_create.argtypes = [ctypes.POINTER(capi.PlanDesc), ctypes.POINTER(ctypes.c_void_p)]
     L.mgx_extract_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
