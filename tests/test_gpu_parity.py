@@ -323,7 +323,8 @@ def test_scalar_windows_equal_per_batch_form(capi, n):
     window of 16 batches, one lane per frame (kernels.hip scalar_pass); a smaller launch computes
     them per batch, one lane per (feature, frame). The same frames through both must give the same
     bits: a ragged 262,157-frame launch (partial batch, partial last windows) against chunks of
-    16,384 frames, every feature, C3's subset, float32 and float64 scalars, the reference-order MFCC,
+    16,384 frames, every feature, C3's subset, time features beside a spectrum-only request (the light
+    kernels, whose records hold only those), float32 and float64 scalars, the reference-order MFCC,
     and non-finite, silent and loud frames among them (a NaN output may differ in its sign bit:
     the formulas are the same, the instructions that propagate the NaN are not)."""
     import torch
@@ -336,7 +337,8 @@ def test_scalar_windows_equal_per_batch_form(capi, n):
     x[200003, :] *= 1e19
     x[F - 1, 0] = float("-inf")
     for kw, feats in (({"scalar_f64": True}, capi.ALL_FEATURES), ({}, capi.ALL_FEATURES), ({}, C3_SET),
-                      ({"scalar_f64": True, "mfcc_reference": True}, capi.ALL_FEATURES)):
+                      ({"scalar_f64": True, "mfcc_reference": True}, capi.ALL_FEATURES),
+                      ({}, ["mfcc", "rms", "zcr"]), ({"scalar_f64": True}, ["amplitudeSpectrum", "energy"])):
         plan = capi.Plan(buffer_size=n, **kw)
         whole = plan.extract_torch(x, feats)
         parts = [plan.extract_torch(x[i:i + chunk].contiguous(), feats) for i in range(0, F, chunk)]
