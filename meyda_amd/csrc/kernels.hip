@@ -1892,9 +1892,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     g1 = b < hi ? b : hi;
   };
   if (N >= 512 && N != 1024 && many && nr >= 2 && nr <= 8 && gridDim.x % nr == 0) {
-    // other N: rank r's weight 2 (R - 1) - r, from 2:1 for the first rank to the last
+    // other N: rank r's weight 5 (R - 1) - 2 r, from 5:3 for the first rank to the last (round 4: 2:1
+    // before; 5:3 measured -1.2 % at N = 2048 and -0.9..-1.7 % at 512, steeper and flatter ones slower)
     const uint64_t q = gridDim.x / nr, r = blockIdx.x / q, i = blockIdx.x % q;
-    auto cum = [&](uint64_t k) { return k * 2 * (nr - 1) - k * (k - 1) / 2; };
+    auto cum = [&](uint64_t k) { return k * 5 * (nr - 1) - k * (k - 1); };  // weights 5 (R - 1) - 2 r
     const uint64_t cs = cum(nr);
     split(ev(ng * cum(r) / cs), r + 1 == nr ? ng : ev(ng * cum(r + 1) / cs), q, i);
   } else if (N == 1024 && many && nr == 4 && (gridDim.x & 3) == 0) {
