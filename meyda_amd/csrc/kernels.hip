@@ -1876,7 +1876,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   const uint64_t nr = (uint64_t)ap->wg_ranks;
   // (unequal shares need many groups per workgroup: with a few each, their rounding unbalances
   // more than the ranks' rates do -- C2's 65,536 frames at N = 512 lost 6 %; and N = 256 lost 4 %)
-  const bool many = ng >= 8 * (uint64_t)gridDim.x;
+  // (12 groups per workgroup: at 8-11 the rank shares' pair rounding cost more than the ranks'
+  // rates gain -- 196,608 frames at N = 512 -5.0 %, 131,072 at 1024 -1.9 % with equal pairs instead;
+  // below 8 equal pairs won by 2-16 %, profiles/r04_rank_shares.txt)
+  const bool many = ng >= 12 * (uint64_t)gridDim.x;
   // Every boundary between two workgroups' ranges falls on an even group (32 frames): the
   // 4-byte scalar outputs of a workgroup then fill whole 128-byte lines (and the 52-byte MFCC
   // and 96-byte loudness records whole lines too), so no output line is written from two
