@@ -12,8 +12,13 @@ constexpr int kMaxMel = 64;
 // scalar_pass), one lane per frame: the window's per-frame inputs (10 8-byte words each, the
 // record's S[0..4], ln2sum, energy, loudness total, zcr | roll_m, loud_max | sharp_sum) wait in
 // device memory, kScalWords words per wave.
-constexpr int kScalBatches = 16;
-constexpr int kScalWords = 10 * 4 * kScalBatches;
+#ifndef MGX_SCAL_BATCHES
+#define MGX_SCAL_BATCHES 16
+#endif
+constexpr int kScalBatches = MGX_SCAL_BATCHES;
+// word c of the window's frame l (l = 4 batch + frame, < 4 kScalBatches) at c * 64 + l
+static_assert(4 * kScalBatches <= 64, "a window's frames are lanes of one wave");
+constexpr int kScalWords = 10 * 64;
 constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
