@@ -1878,7 +1878,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // more than the ranks' rates do -- C2's 65,536 frames at N = 512 lost 6 %; and N = 256 lost 4 %)
   // (12 groups per workgroup: at 8-11 the rank shares' pair rounding cost more than the ranks'
   // rates gain -- 196,608 frames at N = 512 -5.0 %, 131,072 at 1024 -1.9 % with equal pairs instead;
-  // below 8 equal pairs won by 2-16 %, profiles/r04_rank_shares.txt)
+  // below 8 equal pairs won by 2-16 %, profiles/r04_tuning.txt)
   const bool many = ng >= 12 * (uint64_t)gridDim.x;
   // Every boundary between two workgroups' ranges falls on an even group (32 frames): the
   // 4-byte scalar outputs of a workgroup then fill whole 128-byte lines (and the 52-byte MFCC
