@@ -668,15 +668,17 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
 int mgx_plan_destroy(mgx_plan* p) {
   if (!p) return MGX_OK;
   (void)hipSetDevice(p->d.device);
+  // every launch that used the plan's memory is done first: the plan's own streams, then the
+  // caller streams' scratch events (launches on s_comp record none)
+  if (p->s_copy) (void)hipStreamSynchronize(p->s_copy);
+  if (p->s_comp) (void)hipStreamSynchronize(p->s_comp);
+  for (auto& r : p->chain_rings) (void)hipEventSynchronize(r.done);
   if (p->dev) (void)hipFree(p->dev);
   for (auto& r : p->chain_rings) {
-    (void)hipEventSynchronize(r.done);
     (void)hipEventDestroy(r.done);
     (void)hipFree(r.scal);
     if (r.rows) (void)hipFree(r.rows);
   }
-  if (p->s_copy) (void)hipStreamSynchronize(p->s_copy);
-  if (p->s_comp) (void)hipStreamSynchronize(p->s_comp);
   for (int i = 0; i < 2; ++i) {
     if (p->s_frames[i]) (void)hipFree(p->s_frames[i]);
     if (p->s_out[i]) (void)hipFree(p->s_out[i]);
@@ -789,7 +791,9 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
     }
     a.chain_rows = ring->rows;
   }
-  hipEvent_t ring_done = ring->done;
+  // (a launch on the plan's own compute stream records no event: destroy synchronises that
+  // stream, and the small host path saves the record's ~1 us per call)
+  hipEvent_t ring_done = stream == static_cast<void*>(p->s_comp) ? nullptr : ring->done;
   if (done) {
     a.done_flag = const_cast<uint32_t*>(done);
     a.done_count = p->d_done_count;
