@@ -477,6 +477,10 @@ struct mgx_plan {
   // the small path's completion word (KernelArgs::done_flag): a mapped host word, the device
   // counter of finished waves and the launch sequence number
   uint32_t* h_done = nullptr;
+  // the device addresses of h_in, h_out and h_done (looked up once per allocation, not per call)
+  void* d_in_map = nullptr;
+  void* d_out_map = nullptr;
+  uint32_t* d_done_map = nullptr;
   uint32_t* d_done_count = nullptr;
   uint32_t done_seq = 0;
   float* h_in = nullptr;
@@ -887,6 +891,8 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
     const size_t want = std::max<size_t>(in_bytes, 16 * (size_t)n * sizeof(float));
     e = hipHostMalloc(reinterpret_cast<void**>(&p->h_in), want, hipHostMallocMapped | hipHostMallocCoherent);
     if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(small batch frames)");
+    e = hipHostGetDevicePointer(&p->d_in_map, p->h_in, 0);
+    if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer(small batch frames)");
     p->h_in_bytes = want;
   }
   if (p->h_out_bytes < out_bytes) {
@@ -895,15 +901,14 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
     p->h_out_bytes = 0;
     e = hipHostMalloc(reinterpret_cast<void**>(&p->h_out), out_bytes, hipHostMallocMapped | hipHostMallocCoherent);
     if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(small batch outputs)");
+    e = hipHostGetDevicePointer(&p->d_out_map, p->h_out, 0);
+    if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer(small batch outputs)");
     p->h_out_bytes = out_bytes;
   }
   int rc = fill(p->h_in);
   if (rc) return rc;
-  void* din = nullptr;
-  void* dout = nullptr;
-  e = hipHostGetDevicePointer(&din, p->h_in, 0);
-  if (e == hipSuccess) e = hipHostGetDevicePointer(&dout, p->h_out, 0);
-  if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
+  void* const din = p->d_in_map;
+  void* const dout = p->d_out_map;
   mgx_outputs d{};
   const mgx_outputs h = [&] {  // the same layout, host addresses
     mgx_outputs r{};
@@ -945,11 +950,14 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
       (void)hipHostFree(hd);
       return hip_fail(e, "completion counter");
     }
+    e = hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_done_map), hd, 0);
+    if (e != hipSuccess) {
+      (void)hipHostFree(hd);
+      return hip_fail(e, "hipHostGetDevicePointer(completion word)");
+    }
     p->h_done = hd;
   }
-  uint32_t* ddone = nullptr;
-  e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ddone), p->h_done, 0);
-  if (e != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer(completion word)");
+  uint32_t* const ddone = p->d_done_map;
   p->done_seq = p->done_seq + 1 ? p->done_seq + 1 : 1;  // never 0, the word's initial value
   rc = extract_device_impl(p, static_cast<const float*>(din), nframes, &d, p->s_comp, ddone);
   if (rc) {
