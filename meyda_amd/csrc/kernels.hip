@@ -288,6 +288,15 @@ struct KlTab {
 // NT: a non-temporal load (the CHAIN kernels' frames: the power-row ring keeps more of the L2;
 // -0.6..-1.2 % per reference-order launch, profiles/r03_mfcc_tracks.txt. The other kernels keep
 // plain loads: C2's batch stays in the MALL between launches, which nt loads lose)
+// A spectrum output element (amplitude, power, complex: 2-8 KB per frame, written once and never
+// read back): a non-temporal store, which streams past the caches instead of filling them (every
+// output at N = 1024: -8.1..-8.8 % per launch; C2's 1 GiB batch -0.7 %, outputs identical; the same
+// for the scalar, loudness and MFCC outputs, tens of bytes per frame, measured no gain).
+template <class P>
+__device__ __forceinline__ void st_out(P p, float v) {
+  __builtin_nontemporal_store(v, p);
+}
+
 template <bool NT = false>
 __device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))) float* p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -1269,8 +1278,8 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
         auto ci = uniform_ptr(gbl(ap->out.complex_imag) + f * (uint64_t)N);
         for (unsigned i = lane; i < (unsigned)N; i += 64) {
           const float2 zz = i <= L ? buf[i] : buf[N - i];
-          cr[i] = zz.x;
-          ci[i] = i <= L ? zz.y : -zz.y;
+          st_out(&cr[i], zz.x);
+          st_out(&ci[i], i <= L ? zz.y : -zz.y);
         }
       }
       wave_sync();
@@ -1284,14 +1293,14 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   if (valid && ap->out.amplitude_spectrum) {
     auto o = uniform_ptr(gbl(ap->out.amplitude_spectrum) + f * (uint64_t)L);
 #pragma unroll
-    for (int c = 0; c < R; ++c) o[c * 64 + (unsigned)lane] = amp[pa(c * 64 + lane)];
+    for (int c = 0; c < R; ++c) st_out(&o[c * 64 + (unsigned)lane], amp[pa(c * 64 + lane)]);
   }
   if (valid && ap->out.power_spectrum) {
     auto o = uniform_ptr(gbl(ap->out.power_spectrum) + f * (uint64_t)L);
 #pragma unroll
     for (int c = 0; c < R; ++c) {
       const float av = amp[pa(c * 64 + lane)];
-      o[c * 64 + (unsigned)lane] = av * av;  // powerSpectrum.js
+      st_out(&o[c * 64 + (unsigned)lane], av * av);  // powerSpectrum.js
     }
   }
 
