@@ -51,6 +51,9 @@ const uint64_t kHostChunk = 65536;              // frames per host-staging chunk
 // no cross-stream events: one launch and one stream synchronisation per call). Overridden by
 // $MGX_SMALL_BATCH_FRAMES at plan creation (0: always the staged path).
 const uint64_t kSmallBatchFrames = 512;
+// How long the small path spins on its completion word before it blocks on the stream (a
+// 512-frame batch takes ~0.1 ms; a longer wait is a busy device, where blocking frees the core).
+const int kSmallSpinUs = 2000;
 const double kJsPi = 3.141592653589793;        // Math.PI
 const double kJsSqrt1_2 = 0.7071067811865476;  // Math.SQRT1_2
 
@@ -680,7 +683,7 @@ int mgx_plan_destroy(mgx_plan* p) {
   if (p->dev) (void)hipFree(p->dev);
   for (auto& r : p->chain_rings) {
     (void)hipEventDestroy(r.done);
-    (void)hipFree(r.scal);
+    if (r.scal) (void)hipFree(r.scal);
     if (r.rows) (void)hipFree(r.rows);
   }
   for (int i = 0; i < 2; ++i) {
@@ -772,20 +775,24 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
   for (auto& r : p->chain_rings)
     if (r.stream == stream) ring = &r;
   if (!ring) {
-    // kScalWords words for each wave of the largest grid (4 waves per workgroup)
-    uint64_t* scal = nullptr;
-    e = hipMalloc(reinterpret_cast<void**>(&scal), (size_t)p->grid_cap * 4 * mgx::kScalWords * sizeof(uint64_t));
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc(scalar windows)");
     hipEvent_t done = nullptr;
     e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
-    if (e != hipSuccess) {
-      (void)hipFree(scal);
-      return hip_fail(e, "hipEventCreate(stream scratch)");
-    }
-    p->chain_rings.push_back({stream, scal, nullptr, done});
+    if (e != hipSuccess) return hip_fail(e, "hipEventCreate(stream scratch)");
+    p->chain_rings.push_back({stream, nullptr, nullptr, done});
     ring = &p->chain_rings.back();
   }
-  a.scal_rows = ring->scal;
+  if (a.scal_defer) {
+    // kScalWords words for each wave of the largest grid (4 waves per workgroup), allocated by the
+    // first launch on the stream that defers its scalars (a small or time-only launch never does)
+    if (!ring->scal) {
+      e = hipMalloc(reinterpret_cast<void**>(&ring->scal), (size_t)p->grid_cap * 4 * mgx::kScalWords * sizeof(uint64_t));
+      if (e != hipSuccess) {
+        ring->scal = nullptr;
+        return hip_fail(e, "hipMalloc(scalar windows)");
+      }
+    }
+    a.scal_rows = ring->scal;
+  }
   if (a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) {
     if (!ring->rows) {
       // 2 FPW x N/2 floats for each wave of the largest grid (4 waves per workgroup)
@@ -797,7 +804,8 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
   }
   // (a launch on the plan's own compute stream records no event: destroy synchronises that
   // stream, and the small host path saves the record's ~1 us per call)
-  hipEvent_t ring_done = stream == static_cast<void*>(p->s_comp) ? nullptr : ring->done;
+  // (a NULL caller stream is never the plan's: s_comp may not exist yet, and then both are NULL)
+  hipEvent_t ring_done = (p->s_comp != nullptr && stream == static_cast<void*>(p->s_comp)) ? nullptr : ring->done;
   if (done) {
     a.done_flag = const_cast<uint32_t*>(done);
     a.done_count = p->d_done_count;
@@ -826,8 +834,9 @@ int ensure_host_staging(mgx_plan* p, uint64_t chunk, size_t out_bytes) {
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if (!p->s_copy) {
+    // (the small host path may have created s_comp already: it is created once, never replaced)
     e = hipStreamCreateWithFlags(&p->s_copy, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->s_comp, hipStreamNonBlocking);
+    if (e == hipSuccess && !p->s_comp) e = hipStreamCreateWithFlags(&p->s_comp, hipStreamNonBlocking);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
       e = hipEventCreateWithFlags(&p->ev_loaded[i], hipEventDisableTiming);
       if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_done[i], hipEventDisableTiming);
@@ -967,7 +976,8 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
   // The last wave of the launch releases done_seq to the host word after every output store is
   // visible (kernels.hip done_signal): polling it returns ~9 us sooner than waiting for the
   // stream (tools/ubench/small_latency.hip). Past 20 ms (a busy device) the wait blocks on the
-  // stream instead, which also reports a failed launch.
+  // stream instead, which also reports a failed launch. The spin pauses the core between reads
+  // (a contended device leaves N-API worker threads waiting here) and gives up after kSmallSpinUs.
   {
     const auto t0 = std::chrono::steady_clock::now();
     bool seen = false;
@@ -976,7 +986,8 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
         seen = true;
         break;
       }
-      if ((spins & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+      __builtin_ia32_pause();
+      if ((spins & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSmallSpinUs)) break;
     }
     if (!seen) {
       e = hipStreamSynchronize(p->s_comp);

@@ -313,6 +313,47 @@ def test_small_host_batches_equal_staged_path(capi, n):
             assert np.array_equal(a2[k].view(np.uint8), b2[k].view(np.uint8)), (F, k, "second call")
 
 
+def test_small_and_staged_calls_alternate_on_one_plan(capi):
+    """One plan serving small host batches (its own compute stream, created by the small path) and
+    staged ones (which create the copy stream beside it) in turn, then destroyed: the staged path must
+    reuse the small path's stream rather than replace it (a replaced stream was never synchronised or
+    destroyed), and every call gives the same bits as a fresh plan's."""
+    n = 1024
+    rng = np.random.default_rng(7)
+    feats = capi.ALL_FEATURES
+    ref = capi.Plan(buffer_size=n, scalar_f64=True)
+    p = capi.Plan(buffer_size=n, scalar_f64=True)
+    for F in (1, 600, 3, 2000, 64, 513, 1):
+        x = rng.uniform(-1, 1, (F, n)).astype(np.float32)
+        a, b = p.extract(x, feats), ref.extract(x, feats)
+        for k in a:
+            assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), (F, k)
+    p.close()
+    ref.close()
+
+
+def test_destroy_right_after_default_stream_launch(capi):
+    """mgx_plan_destroy waits for every launch that used the plan (include/meyda_gpu.h), also a large
+    batch launched on the default (NULL) stream before the plan had a stream of its own: its scratch
+    completion event is recorded, and destroy waits on it before freeing the tables."""
+    import torch
+    n = 1024
+    x = torch.empty(262144, n, dtype=torch.float32, device="cuda")
+    capi.synth_frames_device(x, 0xD35)
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(3):
+        p = capi.Plan(buffer_size=n)
+        with torch.cuda.stream(torch.cuda.default_stream()):
+            outs.append(p.extract_torch(x, capi.ALL_FEATURES))
+        p.close()  # right away: the launch is still running
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        for k in o:
+            assert torch.equal(o[k], outs[0][k]), k
+    assert torch.isfinite(outs[0]["spectralCentroid"]).all()
+
+
 C3_SET = ["spectralCentroid", "spectralFlatness", "spectralSlope", "spectralRolloff", "spectralSpread",
           "spectralSkewness", "spectralKurtosis", "loudness", "perceptualSpread", "perceptualSharpness"]
 
