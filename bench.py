@@ -34,8 +34,8 @@ line: its shards' rate, and at N > 1 its gather-inclusive rate, `vs_shards` and 
 communicator's view (at N = 1 the gather is reported as skipped).
 
 A gather that fails or passes its deadline leaves `value` (the shards) measured: rank 0
-still prints the line with the gather's status and the process exits 0, unless
---strict-gather asks for exit status 3 in that case.
+still prints the line with the gather's status, then the process exits with status 3 -- a
+broken RCCL path is a failed run. --allow-gather-failure (a shards-only run) exits 0 instead.
 """
 import argparse
 import concurrent.futures as cf
@@ -95,8 +95,10 @@ def parse(argv=None):
     ap.add_argument("--chunks", type=int, default=0, help="N > 1: gather pipeline depth (0 = automatic)")
     ap.add_argument("--gather-timeout", type=float, default=60.0,
                     help="N > 1: deadline (s) of each gather phase; past it rank 0 reports the shards alone")
-    ap.add_argument("--strict-gather", action="store_true",
-                    help="N > 1: exit status 3 (after the line is printed) when a gather failed or timed out")
+    ap.add_argument("--allow-gather-failure", action="store_true",
+                    help="N > 1: exit 0 even when a gather failed or timed out (the line still reports the "
+                         "shards and the gather's status); by default such a run exits with status 3")
+    ap.add_argument("--strict-gather", action="store_true", help=argparse.SUPPRESS)  # the default since round 5
     ap.add_argument("--allow-shared-gpu", action="store_true",
                     help="rehearsal only: ranks may share a GPU (RCCL refuses that, so no gather)")
     ap.add_argument("--no-every-output", action="store_true",
@@ -164,6 +166,21 @@ def cpu_baseline(n, seconds):
                     "sample": "%d frames (N=%d, all features, seeded noise, the reference's per-buffer structure) "
                               "over %.1f s on %d worker_threads; 1 thread: %.0f frames/s"
                               % (many["frames"], n, many["seconds"], threads, one["value"])})
+        # also os.cpus().length worker_threads -- the whole host, beyond this GPU's share
+        allc = os.cpu_count() or threads
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            aff = allc
+        try:
+            a = node_cpu(n, seconds, allc, timeout_extra=300)
+            out["all_cores"] = {"value": a["value"], "unit": "frames/s", "cores": allc, "schedulable_cpus": aff,
+                                "kind": "js-restatement",
+                                "sample": "%d frames (N=%d, all features) over %.1f s on %d worker_threads "
+                                          "(os.cpus().length; %d CPUs in this process's affinity mask)"
+                                          % (a["frames"], n, a["seconds"], allc, aff)}
+        except Exception as e:  # a report, never the measurement itself
+            out["all_cores"] = {"value": None, "cores": allc, "note": "failed: %r" % (e,)}
         cfgs = {}
         for key, (cn, fset, what) in CPU_SETS.items():
             try:
@@ -336,6 +353,9 @@ def pmc_live(n, F, precision):
               "valu": ("all", 26, "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 "
                                   "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS"),
               "mfma": ("all", 26, mfma),
+              # VALU-busy (faithful mode is FP64-VALU bound): SQ_ACTIVE_INST_* count quad-cycles
+              # of issue summed over the waves; GRBM_GUI_ACTIVE the kernel's cycles summed over the 8 XCDs
+              "busy": ("all", 26, "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"),
               # config C4 exactly (40 mel bands, mfcc alone): north_star's MFMA utilisation of that line
               "mfma_c4": ("mfcc", 40, mfma)}
     got = {}
@@ -366,6 +386,15 @@ def pmc_live(n, F, precision):
             "f64_per_frame": sum(v[k] for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
                                                 "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")) / F,
             "lds_per_frame": v["SQ_INSTS_LDS"] / F}
+    b = got["busy"]
+    simds = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    kcyc = b["GRBM_GUI_ACTIVE"] / 8.0  # the kernel's cycles (per XCD)
+    valu["busy_counters"] = {k: b[k] for k in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY", "SQ_BUSY_CYCLES",
+                                                  "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE")}
+    # issue quad-cycles x 4 over (kernel cycles x SIMDs): the fraction of SIMD cycles that issued VALU work
+    valu["valu_busy_measured"] = 4.0 * b["SQ_ACTIVE_INST_VALU"] / (kcyc * simds)
+    valu["any_busy_measured"] = 4.0 * b["SQ_ACTIVE_INST_ANY"] / (kcyc * simds)
+    valu["busy_simds"] = simds
     valu["mfma_f64"] = _mfma_pass(got["mfma"])
     valu["mfma_f64_c4"] = dict(_mfma_pass(got["mfma_c4"]), config="C4: 40 mel bands x 13 MFCC, mfcc alone")
     note = ("live: rocprofv3 --pmc passes of this run over tools/pmc_probe.py (%d frames x N=%d, same features); "
@@ -514,8 +543,8 @@ class Watchdog:
     """Deadline of one gather phase of a multi-GPU run. The RCCL path cannot be interrupted
     once a peer is missing (a rank that failed, a message never posted), so when the deadline
     passes rank 0 prints the line it already has -- the shards measured without the gather,
-    with the gather's status -- and every rank leaves (exit_code(): 0 unless --strict-gather,
-    so the launcher does not tear rank 0 down before it has printed)."""
+    with the gather's status -- and every rank leaves with gather_exit_code() (3, or 0 under
+    --allow-gather-failure); rank 0 prints before it leaves, so the line is never lost."""
 
     def __init__(self, seconds, emit, code):
         import threading
@@ -535,6 +564,15 @@ class Watchdog:
 
     def cancel(self):
         self.t.cancel()
+
+
+def gather_exit_code(args, statuses):
+    """Exit status of a run from its gather phases' statuses: 0 when every gather that ran
+    reports "ok" (or none ran: N = 1, --no-gather, shared GPUs), else 3 -- a failed or timed-out
+    RCCL gather fails the run even though the shards' `value` was measured -- unless
+    --allow-gather-failure asked for a shards-only run."""
+    bad = [s for s in statuses if s is not None and s != "ok"]
+    return 0 if not bad or getattr(args, "allow_gather_failure", False) else 3
 
 
 def launch_ms(stats):
@@ -613,6 +651,11 @@ def main():
         el5, km5, st5 = measure_shards(w5, devs, args, dist)
         c5 = c5_field(gpus, args.c5_frames, el5, km5, st5, args.steps, gather_on, args.chunks)
         line_box["c5"] = c5
+        if mode == "one" and not args.no_mfcc_exact and args.precision != "fast":
+            d0 = devs.devs[0]
+            c5["mfcc_exact"] = mfcc_exact_of(c5, timed_launches(
+                args, devs, capi.Plan(buffer_size=C5_N, precision=args.precision, mfcc_reference=True, device=d0),
+                FEATURES, 4 * C5_N + 4 * OUT_FLOATS, w5.frames[d0]))
     if mode == "one":
         line_box.update(secondary(args, head.plans[devs.devs[0]], head.frames[devs.devs[0]], devs, n, F))
 
@@ -625,7 +668,7 @@ def main():
         print(json.dumps(build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, gather,
                                     line_box)), flush=True)
 
-    code = 3 if args.strict_gather else 0
+    code = gather_exit_code(args, ["failed"])  # what a failed or timed-out gather phase exits with
     phases = []
     if gather_on:
         phases.append((head, gather))
@@ -650,6 +693,35 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+    rc = gather_exit_code(args, [t.get("status") for _, t in phases])
+    if rc:
+        print("bench.py: a gather did not complete (%s); exit %d (--allow-gather-failure: 0)"
+              % ([t.get("status") for _, t in phases], rc), file=sys.stderr, flush=True)
+        sys.exit(rc)
+
+
+def timed_launches(args, devs, p, feats, bytes_per_frame, fr):
+    """One plan's launches over the frames `fr` on devs' first device, timed as `value`'s are
+    (settle, warmup, the pipelined timed steps, then the serialised launches for kernel_ms)."""
+    dev = devs.devs[0]
+    Fx = fr.shape[0]
+    sets = [p.alloc_outputs(Fx, feats, device="cuda:%d" % dev) for _ in range(2)]
+
+    def st(k):
+        p.extract_device(fr.data_ptr(), Fx, sets[k & 1][1], devs.stream(dev, k).cuda_stream)
+    settle(st, devs, args.settle_ms)
+    el, km, stats = run_mode(st, devs, args.steps, args.warmup, None)
+    alone = launch_ms(stats)
+    return {"value": Fx * args.steps / el, "unit": "frames/s", "kernel_ms": alone, "period_ms": km,
+            "bytes_per_frame": bytes_per_frame,
+            "roofline_frac": Fx * bytes_per_frame / (alone * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frac_pipelined": Fx * bytes_per_frame / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
+def mfcc_exact_of(base, exact):
+    """A config's reference-order MFCC timing (MGX_FLAG_MFCC_REFERENCE) beside its default one."""
+    return dict(exact, flag="MGX_FLAG_MFCC_REFERENCE (mfcc.js:53-93 in the reference's own order)",
+                cost_vs_config_kernel=exact["kernel_ms"] / base["kernel_ms"] - 1.0)
 
 
 def secondary(args, plan, frames, devs, n, F):
@@ -660,18 +732,7 @@ def secondary(args, plan, frames, devs, n, F):
     dev = devs.devs[0]
 
     def timed(p, feats, bytes_per_frame, fr=frames):
-        Fx = fr.shape[0]
-        sets = [p.alloc_outputs(Fx, feats) for _ in range(2)]
-
-        def st(k):
-            p.extract_device(fr.data_ptr(), Fx, sets[k & 1][1], devs.stream(dev, k).cuda_stream)
-        settle(st, devs, args.settle_ms)
-        el, km, stats = run_mode(st, devs, args.steps, args.warmup, None)
-        alone = launch_ms(stats)
-        return {"value": Fx * args.steps / el, "unit": "frames/s", "kernel_ms": alone, "period_ms": km,
-                "bytes_per_frame": bytes_per_frame,
-                "roofline_frac": Fx * bytes_per_frame / (alone * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "frac_pipelined": Fx * bytes_per_frame / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        return timed_launches(args, devs, p, feats, bytes_per_frame, fr)
     if not args.no_fast and args.precision != "fast":
         # the fp32-butterfly mode beside the faithful one (same features and frames)
         out["fast_mode"] = dict(timed(capi.Plan(buffer_size=n, precision="fast", device=dev), FEATURES,
@@ -686,6 +747,10 @@ def secondary(args, plan, frames, devs, n, F):
         # BASELINE config C4 exactly: 40-band mel + 13 MFCC, nothing else (4,148 B/frame)
         out["c4"] = dict(timed(capi.Plan(buffer_size=n, precision=args.precision, num_mel_bands=40, device=dev),
                                ["mfcc"], 4 * n + 4 * 13), features=["mfcc"], mel_bands=40, mfcc_coeffs=13)
+        if not args.no_mfcc_exact and args.precision != "fast":
+            out["c4"]["mfcc_exact"] = mfcc_exact_of(out["c4"], timed(
+                capi.Plan(buffer_size=n, precision=args.precision, num_mel_bands=40, mfcc_reference=True, device=dev),
+                ["mfcc"], 4 * n + 4 * 13))
     if not args.no_c3:
         # BASELINE config C3: spectral* + loudness + perceptual (4,232 B/frame)
         out["c3"] = dict(timed(plan, C3_FEATURES, 4 * n + 4 * (7 + 25 + 2)), features=C3_FEATURES)
@@ -725,6 +790,33 @@ def secondary(args, plan, frames, devs, n, F):
                 out[key]["cpu_baseline"] = c
         if "latency" in out and "c1" in cb.get("configs", {}):
             out["latency"]["cpu_c1_us_per_call"] = cb["configs"]["c1"].get("value")
+    return out
+
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector and matrix share the pipe): 1,024 SIMDs x 32 FLOP/clk x 2.4 GHz
+
+
+def roofline_fp64(n, F, kernel_ms, valu, precision):
+    """The second roofline SURVEY §8(d) asks for beside the HBM one: the FFT's algorithmic flops
+    (5 N log2 N per frame, the radix-2 count) over the kernel's launch duration against the FP64
+    peak, and the SIMD cycles the kernel issued VALU work in (measured, rocprofv3 PMC), with the
+    limit that binds named. Faithful mode computes every butterfly in f64 and converts every stage
+    to f32 and back (jsfft's Float32Array stores), so its FP64-pipe issue, not HBM, is the bound."""
+    flop = 5.0 * n * np.log2(n)
+    tf = F * flop / (kernel_ms * 1e-3) / 1e12
+    out = {"bound": "fp64" if precision == "faithful" else "valu", "unit": "TFLOP/s",
+           "fft_flop_per_frame": flop, "achieved": tf, "peak": FP64_PEAK_TFLOPS, "frac": tf / FP64_PEAK_TFLOPS,
+           "kernel_ms": kernel_ms,
+           "note": "algorithmic FFT flops only (5 N log2 N per frame); the faithful butterflies also issue two f32<->f64 "
+                   "conversions per value and stage, which occupy the same FP64 pipe and are not counted as flops"}
+    if valu:
+        for k in ("valu_busy_measured", "any_busy_measured", "est_valu_busy", "est_fp64_cvt_busy"):
+            if k in valu:
+                out[k] = valu[k]
+        out["binding"] = ("FP64-pipe VALU issue: %.0f f64 + %.0f f32<->f64 conversion instructions of %.0f VALU per frame; "
+                          "the kernel issues VALU work in %.0f %% of its SIMD cycles (measured), HBM at the roofline "
+                          "fraction above" % (valu["f64_per_frame"], valu["cvt_per_frame"], valu["instr_per_frame"],
+                                              100.0 * valu.get("valu_busy_measured", float("nan"))))
     return out
 
 
@@ -803,6 +895,7 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
                      "step_event_ms": stats_s,
                      "bytes_per_frame": bytes_per_frame},
     }
+    line["roofline_fp64"] = roofline_fp64(n, F, kernel_ms, valu, args.precision)
     if gpus > 1:
         line["gather"] = gather if gather is not None else {"status": "off (--no-gather or shared GPUs)"}
     if valu:

@@ -214,3 +214,63 @@ def test_bench_line_carries_every_config():
     c4 = line["valu"]["mfma_f64_c4"]
     assert abs(c4["tflops"] - 512 * 655360.0 / 0.5e-3 / 1e12) < 1e-9 and c4["peak_tflops"] == 78.6
     assert line["roofline"]["traffic"] == 1.13e9 and line["roofline"]["kernel_ms"] == 0.6
+
+
+def test_failed_gather_fails_the_run():
+    """At N > 1 a gather that failed or passed its deadline makes bench.py exit non-zero (status 3)
+    after rank 0 has printed the line with the shards and the gather's status; a run whose gathers
+    all completed, or a run with none (N = 1, --no-gather), exits 0; --allow-gather-failure keeps a
+    shards-only run at 0."""
+    import bench
+    args = bench.parse([])
+    assert not args.allow_gather_failure
+    assert bench.gather_exit_code(args, []) == 0
+    assert bench.gather_exit_code(args, [None]) == 0
+    assert bench.gather_exit_code(args, ["ok", "ok"]) == 0
+    assert bench.gather_exit_code(args, ["ok", "timed out"]) == 3
+    assert bench.gather_exit_code(args, ["failed on rank 3: RuntimeError('ncclRecv')"]) == 3
+    assert bench.gather_exit_code(args, ["not run"]) == 3  # a phase that never started is not a success
+    lenient = bench.parse(["--allow-gather-failure"])
+    assert bench.gather_exit_code(lenient, ["timed out"]) == 0
+
+
+def test_bench_line_carries_fp64_roofline_and_all_core_cpu_baseline(monkeypatch):
+    """the faithful path is FP64-bound, so the line reports the FP64 roofline (the FFT's
+    algorithmic 5 N log2 N flops per frame against the 78.6 TFLOP/s FP64 peak, with the measured
+    VALU-busy fraction and the binding limit named) beside the HBM one; and BASELINE.md's CPU baseline
+    at os.cpus().length worker_threads beside the per-GPU share, with both counts stated."""
+    import types
+
+    import bench
+    args = types.SimpleNamespace(steps=20, warmup=5, precision="faithful", single_stream=False)
+    st = {"launch_alone_mean_ms": 0.6, "launch_serial_ms": 0.6}
+    mf = {"instr_per_launch": 1.0, "flop_per_launch": 512.0, "busy_cycles_per_launch": 1.0, "gui_active_cycles": 1.0}
+    valu = {"instr_per_frame": 1160.0, "cvt_per_frame": 394.0, "f64_per_frame": 438.0, "lds_per_frame": 92.0,
+            "valu_busy_measured": 0.9, "any_busy_measured": 1.2, "mfma_f64": dict(mf), "mfma_f64_c4": dict(mf)}
+    line = bench.build_line(args, 1, "one", [], 262144, 1024, 4.5e8, 0.0116, 0.58, st, None,
+                            {"pmc": (1.13e9, valu, "note")})
+    r = line["roofline_fp64"]
+    assert r["fft_flop_per_frame"] == 5 * 1024 * 10 and r["peak"] == 78.6 and r["bound"] == "fp64"
+    assert abs(r["achieved"] - 262144 * 51200 / 0.6e-3 / 1e12) < 1e-9
+    assert abs(r["frac"] - r["achieved"] / 78.6) < 1e-12
+    assert r["valu_busy_measured"] == 0.9 and "FP64-pipe" in r["binding"] and "est_fp64_cvt_busy" in r
+    assert line["roofline"]["bound"] == "hbm"  # the contract's roofline stays the HBM one
+    # without counters (N > 1, --no-pmc) the flop roofline is still there
+    bare = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, st, None, {})
+    assert bare["roofline_fp64"]["frac"] > 0 and "binding" not in bare["roofline_fp64"]
+
+    calls = []
+
+    def fake_node(n, seconds, threads, fset="all", timeout_extra=120):
+        calls.append((n, fset, threads))
+        return {"value": 1000.0 * threads, "frames": 64 * threads, "seconds": seconds, "cpu_model": "cpu",
+                "logical_cpus": 8, "node": "v12", "us_per_call": 11.0, "calls": 1000}
+    monkeypatch.setattr(bench, "node_cpu", fake_node)
+    monkeypatch.setattr(bench, "cpu_port_c", lambda n, s, t: {"value": 1.0, "cores": t, "kind": "port-c"})
+    import shutil
+    monkeypatch.setattr(shutil, "which", lambda _: "/usr/bin/node")
+    cb = bench.cpu_baseline(1024, 0.1)
+    allc = os.cpu_count()
+    assert cb["cores"] == min(bench.CPU_THREADS, allc) and cb["all_cores"]["cores"] == allc
+    assert cb["all_cores"]["value"] == 1000.0 * allc and "schedulable_cpus" in cb["all_cores"]
+    assert (1024, "all", allc) in calls and cb["one_thread"] == 1000.0
