@@ -488,6 +488,9 @@ def measure_gather(wl, devs, args, dist, mode, rank, world, gpus, out):
     comm = group.comm_info()
     out["rccl_comm"] = {"ranks": comm[0], "rank": comm[1], "device": comm[2], "group_ranks": group.nranks,
                         "local_ranks": group.num_local}
+    out["transport"] = ("ipc rehearsal (MGX_GROUP_TRANSPORT=ipc: hipIpc-mapped transfer buffers + a shared-memory "
+                        "mailbox in place of ncclSend/ncclRecv)" if os.environ.get("MGX_GROUP_TRANSPORT") == "ipc"
+                        else "rccl")
     if group.nranks != gpus or comm[0] != gpus or comm[2] != d0 or comm[1] != group.first_local:
         raise RuntimeError("the RCCL communicator reports %s for a %d-GPU job on device %d" % (comm, gpus, d0))
     out["status"] = "running"
@@ -636,7 +639,10 @@ def main():
         raise SystemExit("bench.py: ranks share a GPU: %s" % placement)
     n, F = args.n, args.frames
     first = rank if dist else 0  # each rank / device its own shard of one global synthetic stream
-    gather_on = gpus > 1 and not args.no_gather and not shared
+    # (MGX_GROUP_TRANSPORT=ipc: the cross-process rehearsal of the gather, whose ranks may share a GPU --
+    # the chunks move through IPC-mapped buffers instead of RCCL, which refuses two ranks on one device)
+    ipc_rehearsal = os.environ.get("MGX_GROUP_TRANSPORT") == "ipc"
+    gather_on = gpus > 1 and not args.no_gather and (not shared or ipc_rehearsal)
     head = Workload(n, F, devs, first, args.precision)
     el_s, km_s, stats_s = measure_shards(head, devs, args, dist)
     value_s = gpus * F * args.steps / el_s

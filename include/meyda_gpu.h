@@ -267,7 +267,14 @@ int mgx_group_create(const mgx_plan_desc* desc, const int32_t* devices, uint32_t
 
 /* One process per device (e.g. torchrun): rank 0 calls mgx_comm_unique_id and the caller
  * broadcasts the bytes; every rank then calls mgx_group_create_rank with its rank.
- * desc->device is this rank's device. Rank 0 is the root. */
+ * desc->device is this rank's device. Rank 0 is the root.
+ * Test transport across processes: with MGX_GROUP_TRANSPORT=ipc in the environment of every
+ * rank, the id names a POSIX shared-memory mailbox instead of an RCCL communicator, and each
+ * peer chunk reaches the root through hipIpcGetMemHandle / hipIpcOpenMemHandle of the peer's
+ * transfer buffer (a device copy on the root's communication stream, handed over through the
+ * mailbox's per-slot sequence numbers) -- the multi-rank data path across a process boundary,
+ * runnable with every rank on one GPU (RCCL refuses that). $MGX_IPC_TIMEOUT_S (default 60)
+ * bounds each wait for a peer; a missing peer is an MGX_E_DEVICE error, not a hang. */
 int mgx_comm_unique_id(void* id, uint64_t id_bytes);
 int mgx_group_create_rank(const mgx_plan_desc* desc, const void* unique_id, uint32_t nranks, uint32_t rank,
                           mgx_group** out);

@@ -11,10 +11,15 @@
 // kernel on the communication stream. RCCL is loaded at run time (dlopen), so the library
 // has no link-time dependency on it and a one-rank group never touches it.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <unistd.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -230,7 +235,78 @@ int ensure(unsigned char** p, uint64_t* cap, uint64_t bytes, const char* what) {
   return MGX_OK;
 }
 
+// ------------------------------------------------------ the cross-process test transport
+// MGX_GROUP_TRANSPORT=ipc (mgx_group_create_rank): R processes, which may share one GPU, move
+// every chunk through CUDA-style IPC instead of RCCL. The ranks rendezvous on a POSIX shared-memory
+// mailbox named by the group id (mgx_comm_unique_id writes that name in place of an RCCL id in this
+// mode); each peer publishes the hipIpcMemHandle of its transfer buffer there, the root opens it
+// (hipIpcOpenMemHandle) and copies each posted chunk into its staging slot on its communication
+// stream, ahead of the same unpack as the RCCL path. Per peer and transfer slot the mailbox holds
+// two sequence numbers: `posted` (the peer's extraction of the slot's chunk has completed) and
+// `consumed` (the root's copy out of it has completed), which stand in for the completion of an
+// ncclSend / ncclRecv pair. The hand-over waits on the host (a rehearsal transport: the shard,
+// chunk, slot and unpack code of the multi-rank path across processes, on one GPU).
+constexpr uint64_t kIpcMagic = 0x6D67782D69706331ull;  // "mgx-ipc1"
+constexpr uint32_t kIpcMaxRanks = 64;
+constexpr char kIpcTag[] = "mgx-ipc:";
+
+struct IpcRankBox {
+  hipIpcMemHandle_t handle;
+  uint64_t gen;        // bumped each time the peer's transfer buffer is (re)allocated
+  uint64_t posted[2];  // per transfer slot: chunks whose extraction has completed
+  uint64_t consumed[2];
+  int32_t device, pid;
+  uint64_t joined;
+};
+struct IpcMail {
+  uint64_t magic;
+  uint32_t nranks, pad;
+  IpcRankBox r[kIpcMaxRanks];
+};
+
+bool ipc_selected() {
+  const char* t = getenv("MGX_GROUP_TRANSPORT");
+  return t && strcmp(t, "ipc") == 0;
+}
+
+template <class T>
+T ld_acq(const T* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+template <class T>
+void st_rel(T* p, T v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+
+// Spins (pausing, then sleeping) until pred() holds or `seconds` pass; false on the deadline.
+template <class Pred>
+bool ipc_wait(Pred pred, double seconds) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 0;; ++i) {
+    if (pred()) return true;
+    if (i < 4096) {
+      __builtin_ia32_pause();
+    } else {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > seconds) return false;
+      usleep(20);
+    }
+  }
+}
+
+double ipc_timeout_s() {
+  const char* t = getenv("MGX_IPC_TIMEOUT_S");
+  return t && atof(t) > 0 ? atof(t) : 60.0;
+}
+
 }  // namespace
+
+// The cross-process mailbox of one group member (Transport::kIpc).
+struct IpcLink {
+  std::string name;
+  IpcMail* mail = nullptr;
+  uint64_t my_gen = 0;
+  uint64_t seq[2] = {0, 0};  // peer: chunks posted per slot
+  // root: per peer, the mapped transfer buffer, its generation and the chunks consumed per slot
+  std::vector<void*> peer_buf;
+  std::vector<uint64_t> peer_gen;
+  std::vector<uint64_t> peer_seq;  // 2 per peer
+};
 
 // How a peer's chunk reaches the root's staging slot.
 enum class Transport {
@@ -238,6 +314,9 @@ enum class Transport {
   kCopy,      // mgx_group_create_loopback: a device copy on the root's communication stream
   kRcclSelf,  // mgx_group_create_loopback_rccl: ncclSend + ncclRecv to self on a one-rank
               // communicator, on the root's communication stream
+  kIpc,       // mgx_group_create_rank with MGX_GROUP_TRANSPORT=ipc: one process per rank (the
+              // ranks may share a GPU), chunks through IPC-mapped transfer buffers and a
+              // shared-memory mailbox (IpcLink)
 };
 
 struct mgx_group {
@@ -246,8 +325,134 @@ struct mgx_group {
   bool single_process = true;
   Transport transport = Transport::kRccl;
   std::vector<Member> m;  // local ranks, in rank order
-  bool loopback() const { return transport != Transport::kRccl; }  // all ranks on one device
+  IpcLink ipc;            // Transport::kIpc
+  bool loopback() const { return transport == Transport::kCopy || transport == Transport::kRcclSelf; }  // all ranks in this process
 };
+
+namespace {
+
+// Creates (rank 0) or joins the mailbox named by the id, and registers this rank in it.
+int ipc_join(mgx_group* g, const char* id, uint32_t rank) {
+  if (strncmp(id, kIpcTag, sizeof kIpcTag - 1) != 0)
+    return fail(MGX_E_INVALID_ARGUMENT, "MGX_GROUP_TRANSPORT=ipc: the group id was not made by mgx_comm_unique_id in this mode");
+  if (g->nranks > kIpcMaxRanks) return fail(MGX_E_UNSUPPORTED, "the IPC transport holds at most %u ranks", kIpcMaxRanks);
+  IpcLink& L = g->ipc;
+  L.name = std::string("/") + (id + sizeof kIpcTag - 1);
+  const size_t bytes = sizeof(IpcMail);
+  int fd = -1;
+  const double tmo = ipc_timeout_s();
+  if (rank == 0) {
+    fd = shm_open(L.name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0) return fail(MGX_E_DEVICE, "shm_open(%s): %s", L.name.c_str(), strerror(errno));
+    if (ftruncate(fd, (off_t)bytes) != 0) {
+      close(fd);
+      shm_unlink(L.name.c_str());
+      return fail(MGX_E_DEVICE, "ftruncate(mailbox): %s", strerror(errno));
+    }
+  } else if (!ipc_wait([&] { return (fd = shm_open(L.name.c_str(), O_RDWR, 0600)) >= 0; }, tmo)) {
+    return fail(MGX_E_DEVICE, "rank %u: the group mailbox %s never appeared", rank, L.name.c_str());
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return fail(MGX_E_DEVICE, "mmap(mailbox): %s", strerror(errno));
+  L.mail = static_cast<IpcMail*>(p);
+  if (rank == 0) {
+    L.mail->nranks = g->nranks;
+    st_rel(&L.mail->magic, kIpcMagic);
+  } else {
+    // (a peer may map the file before rank 0 has initialised it: wait for the magic word)
+    if (!ipc_wait([&] { return ld_acq(&L.mail->magic) == kIpcMagic; }, tmo))
+      return fail(MGX_E_DEVICE, "rank %u: the group mailbox was never initialised", rank);
+    if (L.mail->nranks != g->nranks) return fail(MGX_E_INVALID_ARGUMENT, "the mailbox is for %u ranks, not %u", L.mail->nranks, g->nranks);
+  }
+  IpcRankBox& me = L.mail->r[rank];
+  me.device = g->m[0].device;
+  me.pid = (int32_t)getpid();
+  st_rel(&me.joined, (uint64_t)1);
+  // every rank present before anyone transfers (the barrier of a communicator's creation)
+  if (!ipc_wait([&] {
+        for (uint32_t r = 0; r < g->nranks; ++r)
+          if (!ld_acq(&L.mail->r[r].joined)) return false;
+        return true;
+      }, tmo))
+    return fail(MGX_E_DEVICE, "rank %u: not every rank joined the group within %.0f s", rank, tmo);
+  if (rank == 0) {
+    L.peer_buf.assign(g->nranks, nullptr);
+    L.peer_gen.assign(g->nranks, 0);
+    L.peer_seq.assign(2 * (size_t)g->nranks, 0);
+  }
+  return MGX_OK;
+}
+
+void ipc_leave(mgx_group* g) {
+  IpcLink& L = g->ipc;
+  for (void* b : L.peer_buf)
+    if (b) (void)hipIpcCloseMemHandle(b);
+  L.peer_buf.clear();
+  if (L.mail) munmap(L.mail, sizeof(IpcMail));
+  L.mail = nullptr;
+  if (!L.name.empty()) shm_unlink(L.name.c_str());  // every rank: whichever leaves first removes the name
+  L.name.clear();
+}
+
+// A peer: publish its transfer buffer's handle after an allocation (before any chunk of the call
+// is posted, so the root never maps a freed buffer: the root consumed every chunk of the last one).
+int ipc_publish(mgx_group* g, Member& m) {
+  IpcRankBox& me = g->ipc.mail->r[m.rank];
+  hipIpcMemHandle_t h;
+  HIP_OK(hipIpcGetMemHandle(&h, m.xfer), "hipIpcGetMemHandle(transfer buffer)");
+  me.handle = h;
+  st_rel(&me.gen, ++g->ipc.my_gen);
+  return MGX_OK;
+}
+
+// A peer, before it extracts into transfer slot sl again: the root has copied the slot's last chunk.
+int ipc_wait_consumed(mgx_group* g, uint32_t rank, int sl) {
+  IpcLink& L = g->ipc;
+  IpcRankBox& me = L.mail->r[rank];
+  if (!ipc_wait([&] { return ld_acq(&me.consumed[sl]) >= L.seq[sl]; }, ipc_timeout_s()))
+    return fail(MGX_E_DEVICE, "rank %u: the root did not take chunk %llu of slot %d", rank, (unsigned long long)L.seq[sl], sl);
+  return MGX_OK;
+}
+
+// A peer: chunk of slot sl extracted (its event complete): post it.
+// ($MGX_IPC_FAIL_RANK, a test hook: that rank never posts, so the root's wait passes its deadline)
+int ipc_post(mgx_group* g, Member& m, int sl) {
+  HIP_OK(hipEventSynchronize(m.ev_comp[sl]), "hipEventSynchronize(chunk)");
+  ++g->ipc.seq[sl];
+  const char* f = getenv("MGX_IPC_FAIL_RANK");
+  if (!(f && atoi(f) == (int)m.rank)) st_rel(&g->ipc.mail->r[m.rank].posted[sl], g->ipc.seq[sl]);
+  return MGX_OK;
+}
+
+// The root: peer p's chunk of slot sl into `dst` (bytes, 0 for an empty chunk) on its communication
+// stream, once posted; marks it consumed when the copy has completed.
+int ipc_take(mgx_group* g, Member& root, uint32_t p, int sl, unsigned char* dst, uint64_t slot, uint64_t bytes) {
+  IpcLink& L = g->ipc;
+  IpcRankBox& box = L.mail->r[p];
+  uint64_t& want = L.peer_seq[2 * (size_t)p + sl];
+  ++want;
+  if (!ipc_wait([&] { return ld_acq(&box.posted[sl]) >= want; }, ipc_timeout_s()))
+    return fail(MGX_E_DEVICE, "root: rank %u never posted chunk %llu of slot %d", p, (unsigned long long)want, sl);
+  if (bytes) {
+    const uint64_t gen = ld_acq(&box.gen);
+    if (gen != L.peer_gen[p]) {  // the peer (re)allocated its transfer buffer: map the new one
+      if (L.peer_buf[p]) (void)hipIpcCloseMemHandle(L.peer_buf[p]);
+      L.peer_buf[p] = nullptr;
+      HIP_OK(hipIpcOpenMemHandle(&L.peer_buf[p], box.handle, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+      L.peer_gen[p] = gen;
+    }
+    HIP_OK(hipMemcpyAsync(dst, static_cast<unsigned char*>(L.peer_buf[p]) + sl * slot, bytes, hipMemcpyDeviceToDevice,
+                          root.s_comm),
+           "hipMemcpyAsync(ipc chunk)");
+    HIP_OK(hipEventRecord(root.ev_comm_done, root.s_comm), "hipEventRecord");
+    HIP_OK(hipEventSynchronize(root.ev_comm_done), "hipEventSynchronize(ipc chunk)");
+  }
+  st_rel(&box.consumed[sl], want);
+  return MGX_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -267,6 +472,15 @@ uint64_t mgx_packed_layout(const mgx_plan_desc* desc, uint32_t mask, uint64_t nu
 
 int mgx_comm_unique_id(void* id, uint64_t id_bytes) {
   if (!id || id_bytes < sizeof(ncclUniqueId)) return fail(MGX_E_INVALID_ARGUMENT, "id buffer must hold %d bytes", MGX_COMM_ID_BYTES);
+  if (ipc_selected()) {  // the test transport: the id names the group's shared-memory mailbox
+    uint64_t r = 0;
+    FILE* f = fopen("/dev/urandom", "rb");
+    if (!f || fread(&r, sizeof r, 1, f) != 1) r = (uint64_t)getpid() * 0x9E3779B97F4A7C15ull ^ (uint64_t)time(nullptr);
+    if (f) fclose(f);
+    memset(id, 0, id_bytes);
+    snprintf(static_cast<char*>(id), id_bytes, "%smgx_ipc_%d_%016llx", kIpcTag, (int)getpid(), (unsigned long long)r);
+    return MGX_OK;
+  }
   Rccl* r = rccl();
   if (!r) return fail(MGX_E_UNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
   ncclUniqueId u;
@@ -372,7 +586,10 @@ int mgx_group_create_rank(const mgx_plan_desc* desc, const void* unique_id, uint
   g->m[0].rank = rank;
   g->m[0].device = desc->device;
   int rc = member_init(g->m[0], *desc);
-  if (!rc && nranks > 1) {
+  if (!rc && nranks > 1 && ipc_selected()) {
+    g->transport = Transport::kIpc;
+    rc = ipc_join(g, static_cast<const char*>(unique_id), rank);
+  } else if (!rc && nranks > 1) {
     Rccl* r = rccl();
     if (!r) {
       rc = fail(MGX_E_UNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
@@ -395,6 +612,7 @@ int mgx_group_create_rank(const mgx_plan_desc* desc, const void* unique_id, uint
 int mgx_group_destroy(mgx_group* g) {
   if (!g) return MGX_OK;
   for (Member& m : g->m) member_free(m);
+  if (g->transport == Transport::kIpc) ipc_leave(g);
   delete g;
   return MGX_OK;
 }
@@ -411,7 +629,11 @@ int mgx_group_comm_info(const mgx_group* g, int32_t* comm_ranks, int32_t* comm_r
   if (!g) return fail(MGX_E_INVALID_ARGUMENT, "group is NULL");
   int32_t n = -1, me = -1, dev = -1;
   const ncclComm_t c = g->m.empty() ? nullptr : g->m[0].comm;
-  if (c) {
+  if (g->transport == Transport::kIpc) {  // the mailbox's own view: every rank that joined it
+    n = (int32_t)g->ipc.mail->nranks;
+    me = (int32_t)g->m[0].rank;
+    dev = g->ipc.mail->r[me].device;
+  } else if (c) {
     Rccl* r = rccl();
     int v;
     if (!r) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
@@ -490,12 +712,19 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
     cmax = std::max(cmax, cn);
   }
   const uint64_t slot = packed_layout(d, mask, cmax, nullptr);
+  const bool ipc = g->transport == Transport::kIpc && R > 1;
   // buffers: non-root 2 packed chunks; root 2 staging slots per peer
   for (Member& m : g->m) {
     HIP_OK(hipSetDevice(m.device), "hipSetDevice");
     const uint64_t need = R == 1 ? 0 : (m.rank == 0 ? 2 * slot * (R - 1) : 2 * slot);
+    // (IPC: the root has taken both slots' last chunks before a peer may replace the buffer it maps)
+    if (ipc && m.rank != 0 && m.xfer_bytes < need)
+      for (int sl = 0; sl < 2; ++sl)
+        if (int rc = ipc_wait_consumed(g, m.rank, sl)) return rc;
+    unsigned char* const before = m.xfer;
     int rc = ensure(&m.xfer, &m.xfer_bytes, need, "hipMalloc(transfer buffers)");
     if (rc) return rc;
+    if (ipc && m.rank != 0 && m.xfer != before && (rc = ipc_publish(g, m))) return rc;
   }
   // Extraction runs on the caller's stream (or the member's own): no cross-stream wait on
   // the compute path. Transfers and the root's scatters run on the communication stream,
@@ -517,7 +746,7 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
     if (nch > 1) HIP_OK(hipStreamWaitEvent(m.s_alt, m.ev_start, 0), "hipStreamWaitEvent");
     if (R > 1) HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_start, 0), "hipStreamWaitEvent");
   }
-  const bool uses_rccl = R > 1 && g->transport != Transport::kCopy;
+  const bool uses_rccl = R > 1 && g->transport != Transport::kCopy && g->transport != Transport::kIpc;
   Rccl* rc_ = uses_rccl ? rccl() : nullptr;
   if (uses_rccl && !rc_) return fail(MGX_E_UNSUPPORTED, "RCCL could not be loaded");
   // one RCCL group of point-to-point calls; on an error after ncclGroupStart the group is
@@ -548,7 +777,11 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
           if (rc) return rc;
         }
       } else {
-        if (c >= 2 || m.xfer_sent[sl]) HIP_OK(hipStreamWaitEvent(st, m.ev_sent[sl], 0), "hipStreamWaitEvent");
+        if (ipc) {  // the root has copied the slot's previous chunk out (the mailbox's `consumed`)
+          if (int rc = ipc_wait_consumed(g, m.rank, sl)) return rc;
+        } else if (c >= 2 || m.xfer_sent[sl]) {
+          HIP_OK(hipStreamWaitEvent(st, m.ev_sent[sl], 0), "hipStreamWaitEvent");
+        }
         if (cn) {
           const mgx_outputs o = packed_outputs(d, m.xfer + sl * slot, mask, cn);
           int rc = mgx_extract_device(m.plan, src, cn, &o, st);
@@ -556,10 +789,26 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
         }
         HIP_OK(hipEventRecord(m.ev_comp[sl], st), "hipEventRecord");
         HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_comp[sl], 0), "hipStreamWaitEvent");
+        if (ipc) {  // posted once extracted (every chunk, an empty one too: the sequence stays aligned)
+          if (int rc = ipc_post(g, m, sl)) return rc;
+        }
       }
     }
     if (R == 1) continue;
-    if (g->loopback()) {
+    if (ipc) {
+      // the root takes every peer's posted chunk into its staging slot (the other ranks' part of
+      // the transfer was their post above)
+      Member& root = g->m[0];
+      if (root.rank == 0) {
+        HIP_OK(hipSetDevice(root.device), "hipSetDevice");
+        for (uint32_t p = 1; p < R; ++p) {
+          uint64_t c0, cn;
+          chunk_of(counts[p], nch, c, &c0, &cn);
+          unsigned char* dst = root.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot;
+          if (int rc = ipc_take(g, root, p, sl, dst, slot, cn ? packed_layout(d, mask, cn, nullptr) : 0)) return rc;
+        }
+      }
+    } else if (g->loopback()) {
       // the test transports: each peer's chunk into the root's staging slot on the root's
       // communication stream, after the peer's extraction of it -- a device copy, or an RCCL
       // send to self matched by a receive from self on the root's one-rank communicator

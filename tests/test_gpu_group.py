@@ -269,3 +269,82 @@ def test_plan_launches_pipelined_on_two_streams(capi, n):
             a = got[k].view(torch.int32) if got[k].dtype == torch.float32 else got[k].view(torch.int64)
             b = want[k].view(torch.int32) if want[k].dtype == torch.float32 else want[k].view(torch.int64)
             assert torch.equal(a, b), (k, i)
+
+
+def _ipc_rank(rank, nranks, uid, n, calls, q):
+    """One process of the cross-process rehearsal (MGX_GROUP_TRANSPORT=ipc, every rank on device 0):
+    its shard of each call's frames through mgx_group_create_rank's group; the root compares the
+    gathered record with one plan's extraction of the whole batch, byte for byte."""
+    import os
+    os.environ["MGX_GROUP_TRANSPORT"] = "ipc"
+    os.environ["MGX_IPC_TIMEOUT_S"] = "60"
+    try:
+        import torch
+        from meyda_amd import capi
+        g = capi.Group(buffer_size=n, rank=rank, nranks=nranks, unique_id=uid, device=0, scalar_f64=True)
+        assert (g.nranks, g.first_local, g.num_local) == (nranks, rank, 1)
+        assert g.comm_info() == (nranks, rank, 0), g.comm_info()
+        plan = capi.Plan(buffer_size=n, scalar_f64=True)
+        feats = FEATS
+        bad = []
+        for F, first, nch in calls:
+            counts = [capi.shard_range(F, nranks, r)[1] for r in range(nranks)]
+            s0 = capi.shard_range(F, nranks, rank)[0]
+            x = torch.empty(counts[rank], n, dtype=torch.float32, device="cuda")
+            capi.synth_frames_device(x, SEED, first_frame=first + s0)
+            got, o = plan.alloc_outputs(F if rank == 0 else 1, feats)
+            for v in got.values():
+                v.fill_(float("nan"))
+            torch.cuda.synchronize()
+            g.extract_device([x.data_ptr()], counts, o if rank == 0 else None, capi.output_mask(o), num_chunks=nch)
+            torch.cuda.synchronize()
+            if rank == 0:
+                xa = torch.empty(F, n, dtype=torch.float32, device="cuda")
+                capi.synth_frames_device(xa, SEED, first_frame=first)
+                want = plan.extract_torch(xa, feats)
+                torch.cuda.synchronize()
+                for k in want:
+                    a = got[k].view(torch.int64) if got[k].dtype == torch.float64 else got[k].view(torch.int32)
+                    b = want[k].view(torch.int64) if want[k].dtype == torch.float64 else want[k].view(torch.int32)
+                    if not torch.equal(a, b):
+                        bad.append((F, nch, k))
+        g.close()
+        q.put((rank, "ok" if not bad else "mismatch %s" % bad[:5]))
+    except Exception as e:  # reported to the parent, which fails the test
+        q.put((rank, "error %r" % (e,)))
+
+
+@pytest.mark.parametrize("n", [1024, 2048])
+def test_ipc_transport_two_processes(capi, n):
+    """The cross-process gather rehearsed on one GPU: two processes, each with its own plan and
+    mgx_group_create_rank group, the chunks moving through hipIpcGetMemHandle / hipIpcOpenMemHandle
+    and a shared-memory mailbox in place of ncclSend / ncclRecv (MGX_GROUP_TRANSPORT=ipc). This is
+    the code a multi-GPU torchrun job runs -- per-rank group creation, ragged shards, the chunk
+    loop over two transfer slots on two compute streams, slot reuse across calls, the root's
+    unpack -- across a process boundary. Three calls: 8 chunks, then fewer frames (slot reuse),
+    then more (the peer reallocates and republishes its transfer buffer); byte-identical to one
+    plan's extraction every time."""
+    import multiprocessing as mp
+    import os
+    os.environ["MGX_GROUP_TRANSPORT"] = "ipc"
+    try:
+        uid = capi.comm_unique_id()
+    finally:
+        del os.environ["MGX_GROUP_TRANSPORT"]
+    assert uid.startswith(b"mgx-ipc:")
+    calls = [(40003, 0, 8), (9001, 50000, 3), (70001, 100000, 8)] if n == 1024 else [(20003, 0, 8), (5001, 30000, 2), (36001, 40000, 8)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ipc_rank, args=(r, 2, uid, n, calls, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = []
+    try:
+        for _ in ps:
+            res.append(q.get(timeout=150))
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert sorted(res) == [(0, "ok"), (1, "ok")], res
