@@ -176,6 +176,10 @@ class Meyda {
     const list = this._featuresToExtract;
     const names = typeof list === 'string' ? [list] : Array.prototype.slice.call(list || []);
     const plugins = names.some((n) => this.featureExtractors[n]);
+    if (!plugins && names.every((n) => GPU_FEATURES.has(n) || n === 'buffer')) {
+      this._flushViews(count, list, names);
+      return;
+    }
     const gpu = names.filter((n) => GPU_FEATURES.has(n) && !this.featureExtractors[n]);
     if (plugins) gpu.push('amplitudeSpectrum', 'complexSpectrum', 'loudness');
     const N = this.bufferSize;
@@ -189,6 +193,58 @@ class Meyda {
       for (const n of new Set(gpu)) this._frame[n] = frameValue(n, r, i, N, this.options.numMfccCoeffs);
       const out = typeof list === 'string' ? this._value(list) : this.get(names);
       this._callback(out);
+    }
+    this.signal = keep;
+    this._frame = null;
+  }
+
+  // flush() for built-in features only: one launch, then each callback gets its frame's values as
+  // views into the batch's result arrays (numbers, and subarrays where get() returns arrays) instead
+  // of per-frame copies and a get() dispatch per buffer. The batch's arrays are fresh per launch, so
+  // a view stays valid after its callback. The queued frames move to the batch (the next process()
+  // starts a new ring), so `signal` -- and 'buffer' -- are views of them, as the buffer each callback
+  // describes. get() inside a callback recomputes that buffer's features.
+  _flushViews(count, list, names) {
+    const N = this.bufferSize, L = N >> 1, nc = this.options.numMfccCoeffs || 13;
+    const frames = this._ring.subarray(0, count * N);
+    this._ring = null;
+    const gpu = Array.from(new Set(names.filter((n) => n !== 'buffer')));
+    const r = gpu.length ? addon.extract(this._plan(), frames, gpu) : {};
+    const take = (name) => {
+      switch (name) {
+        case 'buffer': return (i) => frames.subarray(i * N, i * N + N);
+        case 'loudness': {
+          const sp = r['loudness.specific'], tot = r['loudness.total'];
+          return (i) => ({ specific: sp.subarray(i * 24, i * 24 + 24), total: tot[i] });
+        }
+        case 'mfcc': { const a = r.mfcc; return (i) => a.subarray(i * nc, i * nc + nc); }
+        case 'amplitudeSpectrum': { const a = r.amplitudeSpectrum; return (i) => a.subarray(i * L, i * L + L); }
+        case 'powerSpectrum': { const a = r.powerSpectrum; return (i) => a.subarray(i * L, i * L + L); }
+        case 'complexSpectrum': {
+          const re = r['complexSpectrum.real'], im = r['complexSpectrum.imag'];
+          return (i) => ({ real: re.subarray(i * N, i * N + N), imag: im.subarray(i * N, i * N + N), length: N });
+        }
+        default: { const a = r[name]; return (i) => a[i]; }
+      }
+    };
+    const keep = this.signal;
+    const cb = this._callback;
+    if (typeof list === 'string') {
+      const t = take(list);
+      for (let i = 0; i < count; i++) {
+        this.signal = frames.subarray(i * N, i * N + N);
+        this._frame = null;
+        cb(t(i));
+      }
+    } else {
+      const k = names.length, ts = names.map(take);
+      for (let i = 0; i < count; i++) {
+        this.signal = frames.subarray(i * N, i * N + N);
+        this._frame = null;
+        const out = {};
+        for (let j = 0; j < k; j++) out[names[j]] = ts[j](i);
+        cb(out);
+      }
     }
     this.signal = keep;
     this._frame = null;

@@ -135,6 +135,52 @@ check('batched streaming (batchFrames = 4): callbacks per buffer, in order, equa
   ref.dispose();
 });
 
+check('batched streaming delivers views that outlive their batch; string, buffer, spectra and plugin lists', () => {
+  const N = 512;
+  const list = ['buffer', 'rms', 'amplitudeSpectrum', 'complexSpectrum', 'powerSpectrum', 'mfcc', 'loudness'];
+  const seen = [];
+  const m = new Meyda(ctx, null, N, (feat) => seen.push(feat), { batchFrames: 3 });
+  m.start(list);
+  for (let i = 0; i < 7; i++) m.process(frameOf(g, i));
+  m.stop();
+  assert.strictEqual(seen.length, 7);
+  const ref = new Meyda(ctx, null, N);
+  for (let i = 0; i < 7; i++) {   // every batch's values are still the frame's after later batches
+    ref.process(frameOf(g, i));
+    const r = ref.get(list.filter((n) => n !== 'buffer'));
+    assert.deepStrictEqual(Array.from(seen[i].buffer), Array.from(frameOf(g, i)), 'buffer ' + i);
+    assert.strictEqual(seen[i].rms, r.rms);
+    for (const k of ['amplitudeSpectrum', 'powerSpectrum', 'mfcc']) {
+      assert.ok(seen[i][k] instanceof Float32Array);
+      assert.deepStrictEqual(Array.from(seen[i][k]), Array.from(r[k]), k + ' ' + i);
+    }
+    assert.deepStrictEqual(Array.from(seen[i].complexSpectrum.real), Array.from(r.complexSpectrum.real));
+    assert.deepStrictEqual(Array.from(seen[i].complexSpectrum.imag), Array.from(r.complexSpectrum.imag));
+    assert.strictEqual(seen[i].complexSpectrum.length, N);
+    assert.deepStrictEqual(Array.from(seen[i].loudness.specific), Array.from(r.loudness.specific));
+    assert.strictEqual(seen[i].loudness.total, r.loudness.total);
+  }
+  // a single feature name: the callback gets the bare value, as get('rms') returns it
+  const one = [];
+  const s1 = new Meyda(ctx, null, N, (v) => one.push(v), { batchFrames: 4 });
+  s1.start('rms');
+  for (let i = 0; i < 5; i++) s1.process(frameOf(g, i));
+  s1.stop();
+  assert.deepStrictEqual(one, seen.slice(0, 5).map((x) => x.rms));
+  // a user plugin in the list takes the per-frame path (the plugin sees its frame's m)
+  const pl = [];
+  const s2 = new Meyda(ctx, null, N, (v) => pl.push(v), { batchFrames: 4 });
+  s2.featureExtractors.peak = (n, mm) => Math.max(...mm.ampSpectrum);
+  s2.start(['rms', 'peak']);
+  for (let i = 0; i < 5; i++) s2.process(frameOf(g, i));
+  s2.stop();
+  for (let i = 0; i < 5; i++) {
+    assert.strictEqual(pl[i].rms, seen[i].rms);
+    assert.strictEqual(pl[i].peak, Math.max(...seen[i].amplitudeSpectrum));
+  }
+  [m, ref, s1, s2].forEach((x) => x.dispose());
+});
+
 check('getBatchWav: .wav bytes -> device decode -> features', () => {
   const { wavS16 } = require('./wav');
   const idx = [];
