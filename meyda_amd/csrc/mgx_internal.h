@@ -10,15 +10,15 @@ namespace mgx {
 constexpr int kMaxMel = 64;
 // The scalar features run once per window of kScalBatches batches of a wave (kernels.hip
 // scalar_pass), one lane per frame: the window's per-frame inputs (10 8-byte words each, the
-// record's S[0..4], ln2sum, energy, loudness total, zcr | roll_m, loud_max | sharp_sum) wait in
-// device memory, kScalWords words per wave.
+// record's S[0..4], ln2sum, energy, loudness total, zcr | roll_m, loud_max | sharp_sum) and the
+// frame's index (word 10) wait in device memory, kScalWords words per wave.
 #ifndef MGX_SCAL_BATCHES
 #define MGX_SCAL_BATCHES 16
 #endif
 constexpr int kScalBatches = MGX_SCAL_BATCHES;
 // word c of the window's frame l (l = 4 batch + frame, < 4 kScalBatches) at c * 64 + l
 static_assert(4 * kScalBatches <= 64, "a window's frames are lanes of one wave");
-constexpr int kScalWords = 10 * 64;
+constexpr int kScalWords = 11 * 64;
 constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
@@ -87,6 +87,11 @@ struct KernelArgs {
   int chain_pair;        // the chains of two consecutive batches of a wave run together (8 frames, nfilt <= 31)
   float* chain_rows;     // the chains' power rows: 2 FPW x N/2 floats per wave of the grid (kernels.hip mel_chains)
   uint64_t* scal_rows;   // the scalar window: kScalWords 8-byte words per wave of the grid (kernels.hip scalar_pass)
+  // Run-time schedule (kernels.hip extract_kernel): the batch's groups of 16 frames are dealt in
+  // units of dyn_unit groups from the counter dyn[0] (device memory of the launch's stream, zero
+  // between launches: the last workgroup, counted in dyn[1], resets both); null: static shares.
+  uint32_t* dyn;
+  uint32_t dyn_unit;
 };
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.

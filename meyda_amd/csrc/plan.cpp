@@ -54,6 +54,8 @@ const uint64_t kSmallBatchFrames = 512;
 // How long the small path spins on its completion word before it blocks on the stream (a
 // 512-frame batch takes ~0.1 ms; a longer wait is a busy device, where blocking frees the core).
 const int kSmallSpinUs = 2000;
+// A launch takes the run-time schedule when its workgroups get at least this many units each.
+const uint64_t kDynMinUnits = 2;
 const double kJsPi = 3.141592653589793;        // Math.PI
 const double kJsSqrt1_2 = 0.7071067811865476;  // Math.SQRT1_2
 
@@ -454,6 +456,8 @@ struct mgx_plan {
   int cus = 0;  // compute units of the plan's device
   int chain_groups = 0;  // MGX_FLAG_MFCC_REFERENCE: 8-step groups of the mel chains (chain_schedule)
   int chain_pair = 0;  // ... over two consecutive batches of a wave (8 frames)
+  bool dyn_on = true;  // the run-time schedule (KernelArgs::dyn) for large launches
+  int dyn_unit = 2;    // its unit, in groups of 16 frames
   // Per-stream device scratch, one set per stream a launch used (the launches of one stream run
   // in order, those of two streams may overlap): the scalar windows (kernels.hip scalar_pass) and,
   // for the reference-order MFCC, the mel chains' power rows (mel_chains). Each set's event is
@@ -464,6 +468,7 @@ struct mgx_plan {
     uint64_t* scal;
     float* rows;  // null until a reference-order MFCC launch on the stream
     hipEvent_t done;
+    uint32_t* dyn;  // the run-time schedule's two counters (KernelArgs::dyn), zero between launches
   };
   std::vector<ChainRing> chain_rings;
   // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
@@ -631,6 +636,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
     else if (atoi(gc) > 0) p->grid_cap = atoi(gc);
   }
   if (const char* sb = getenv("MGX_SMALL_BATCH_FRAMES")) p->small_max = (uint64_t)std::max(0, atoi(sb));
+  if (const char* dv = getenv("MGX_DYN")) p->dyn_on = atoi(dv) != 0;
+  if (const char* du = getenv("MGX_DYN_UNIT")) p->dyn_unit = std::max(1, std::min(64, atoi(du)));
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
@@ -684,6 +691,7 @@ int mgx_plan_destroy(mgx_plan* p) {
   for (auto& r : p->chain_rings) {
     (void)hipEventDestroy(r.done);
     if (r.scal) (void)hipFree(r.scal);
+    if (r.dyn) (void)hipFree(r.dyn);
     if (r.rows) (void)hipFree(r.rows);
   }
   for (int i = 0; i < 2; ++i) {
@@ -778,8 +786,28 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
     hipEvent_t done = nullptr;
     e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
     if (e != hipSuccess) return hip_fail(e, "hipEventCreate(stream scratch)");
-    p->chain_rings.push_back({stream, nullptr, nullptr, done});
+    uint32_t* dyn = nullptr;
+    e = hipMalloc(reinterpret_cast<void**>(&dyn), 2 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(dyn, 0, 2 * sizeof(uint32_t), (hipStream_t)stream);
+    if (e != hipSuccess) {
+      if (dyn) (void)hipFree(dyn);
+      (void)hipEventDestroy(done);
+      return hip_fail(e, "schedule counters");
+    }
+    p->chain_rings.push_back({stream, nullptr, nullptr, done, dyn});
     ring = &p->chain_rings.back();
+  }
+  // The run-time schedule (kernels.hip: units of dyn_unit groups of 16 frames from a device-wide
+  // counter) for launches with at least kDynMinUnits units per workgroup, except the reference-order
+  // MFCC's kernels (their paired batches run on consecutive batches of a wave) and the small host
+  // path's launches (a few frames). $MGX_DYN=0 keeps the static shares; $MGX_DYN_UNIT sets the unit.
+  {
+    const uint64_t ng = (nb + 3) / 4;
+    const bool chain_launch = a.chain_groups > 0 && a.need_spectrum && a.need_mfcc;
+    if (!chain_launch && !done && p->dyn_on && ng >= (uint64_t)grid * p->dyn_unit * kDynMinUnits && ng < (1ull << 31)) {
+      a.dyn = ring->dyn;
+      a.dyn_unit = (uint32_t)p->dyn_unit;
+    }
   }
   if (a.scal_defer) {
     // kScalWords words for each wave of the largest grid (4 waves per workgroup), allocated by the
