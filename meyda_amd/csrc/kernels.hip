@@ -1268,7 +1268,10 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
           buf[0] = make_float2(v[r].x, 0.0f);
           buf[L] = make_float2(v[r].y, 0.0f);
         } else {
-          buf[pa_inv(kl(r))] = v[r];  // kl holds pa(bin)
+          // kl holds pa(bin). (opaque: the complex output's 2R addresses, derived here, were otherwise
+          // hoisted out of the frame loop and held in R VGPRs for the whole launch -- spilled at N = 2048
+          // -- by every launch, with or without a complex output)
+          buf[pa_inv(opaque(kl(r)))] = v[r];
         }
       }
       wave_sync();
@@ -1403,12 +1406,15 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
   double* const momt = G::MOM_SLOT ? pbuf : mom;
   if (kMomLds && need_mom) {
-    momt[0 * MS + lane] = P1;
+    // (one lane address per frame, the rows as immediate offsets: five addresses kept across the frame
+    // loop were spilled at N = 2048 and reloaded per frame)
+    double* const mcol = momt + opaque(lane);
+    mcol[0 * MS] = P1;
     if (need_hi) {
-      momt[1 * MS + lane] = P2;
-      momt[2 * MS + lane] = P3;
-      momt[3 * MS + lane] = P4;
-      momt[4 * MS + lane] = (double)l2f;
+      mcol[1 * MS] = P2;
+      mcol[2 * MS] = P3;
+      mcol[3 * MS] = P4;
+      mcol[4 * MS] = (double)l2f;
     }
   }
   // prefix P(k) = sum_{i<k} a_i: lane-exclusive offset + local prefix
