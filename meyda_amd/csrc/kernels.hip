@@ -2189,6 +2189,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         prio_lo<4>();
       }
     }
+    ++it;
   }
   if (kScalDefer && args_ptr()->scal_defer && (it & (kScalBatches - 1)) != 0) {
     // the wave's last window, with fewer than kScalBatches batches
