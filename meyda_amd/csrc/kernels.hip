@@ -1853,15 +1853,23 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   }
   // the run-time schedule's ring of unit indices (KernelArgs::dyn; words 26..28 of the limits table)
   uint32_t* const uring = reinterpret_cast<uint32_t*>(smem + LY::kc_off + 16 * 8) + 26;
-  if (ap->dyn && threadIdx.x == 0) {
-    // this workgroup's first two units (later ones are taken two ahead: the next unit's first frame is
-    // prefetched during the current unit's last one). Vector atomics at device scope: the counter is
-    // shared by the workgroups of every XCD.
+  uint32_t pu0 = 0, pu1 = 0;  // dyn_mode 2: this wave's first two units (lane 0)
+  if (!CHAIN && ap->dyn) {
+    // the first two units (later ones are taken two ahead: the next unit's first frame is prefetched
+    // during the current unit's last one) -- the workgroup's (dyn_mode 1, into the LDS ring) or the
+    // wave's (dyn_mode 2). Vector atomics at device scope: the counter is shared by every XCD.
     uint32_t* const ctr = ap->dyn;
-    const uint32_t u0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t u1 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uring[0] = u0;
-    uring[1] = u1;
+    if (ap->dyn_mode == 2) {
+      if (lane == 0) {
+        pu0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pu1 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else if (threadIdx.x == 0) {
+      const uint32_t u0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t u1 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uring[0] = u0;
+      uring[1] = u1;
+    }
   }
   if (ap->need_spectrum && ap->need_mfcc) {
     const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
@@ -1955,24 +1963,33 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // (profiles/r04_wave_times.txt); units dealt at run time end within about a unit of each other.
   // (group indices as 32-bit values: a launch holds fewer than 2^32 groups of 16 frames -- plan.cpp
   // takes this schedule only below that -- and the SGPRs are scarce at N = 2048)
+  // dyn_mode 2: units of dyn_unit batches taken by each wave on its own (no barrier; the units of
+  // a wave's neighbours may run on other XCDs, so output lines can be written in pieces).
+  // Positions: groups (static, dyn_mode 1: the wave's batch of group p is 4 p + wave) or batches.
   const bool dyn = !CHAIN && args_ptr()->dyn != nullptr;  // (never with the paired-batch chains)
+  const bool wdyn = dyn && args_ptr()->dyn_mode == 2;
   const uint32_t du = dyn ? args_ptr()->dyn_unit : 1u;
   const uint32_t ng32 = (uint32_t)ng;
-  const uint32_t nunits = dyn ? (ng32 + du - 1) / du : 0;
+  const uint32_t npos = wdyn ? (uint32_t)nb : ng32;
+  const uint32_t nunits = dyn ? (npos + du - 1) / du : 0;
   uint32_t uk = 0;      // units this workgroup has run
-  uint32_t ugrab = 0;   // wave 0, lane 0: the unit taken for ring slot (uk + 2) % 3
-  uint32_t gbeg = (uint32_t)g0, gend = (uint32_t)g1, gnext_unit = (uint32_t)g1;  // this unit's groups; the next unit's first
+  uint32_t ugrab = 0;   // lane 0 of wave 0 (of every wave with dyn_mode 2): the unit taken two ahead
+  uint32_t unx = 0;     // dyn_mode 2: the wave's next unit
+  uint32_t gbeg = (uint32_t)g0, gend = (uint32_t)g1, gnext_unit = (uint32_t)g1;  // this unit's positions; the next unit's first
   // (unit indices read from LDS are made wave-uniform: the schedule's state then lives in SGPRs)
   auto uread = [&](int i) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)uring[i]); };
+  auto urd = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
   if (dyn) {
-    const uint32_t u = uread(0), un = uread(1);
+    const uint32_t u = wdyn ? urd(pu0) : uread(0), un = wdyn ? urd(pu1) : uread(1);
     gbeg = u * du;
-    gend = u < nunits ? (gbeg + du < ng32 ? gbeg + du : ng32) : gbeg;
-    gnext_unit = un < nunits ? un * du : ng32;
-    if (wave == 0 && lane == 0 && u < nunits)
+    gend = u < nunits ? (gbeg + du < npos ? gbeg + du : npos) : gbeg;
+    gnext_unit = un < nunits ? un * du : npos;
+    unx = un;
+    if ((wdyn ? lane == 0 : (wave == 0 && lane == 0)) && u < nunits)
       ugrab = __hip_atomic_fetch_add(args_ptr()->dyn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  const uint64_t b0 = (uint64_t)gbeg * 4 + wave;
+  auto bat = [&](uint32_t p) -> uint64_t { return wdyn ? (uint64_t)p : (uint64_t)p * 4 + wave; };
+  const uint64_t b0 = bat(gbeg);
   // Loads are unconditional (the frame index is clamped; results of frames past the end
   // are never stored), so they issue back to back with no branches or waits between them.
   // With G::PREFETCH the next frame of the wave is loaded while this one is processed.
@@ -2010,24 +2027,33 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   for (uint32_t g = gbeg;; ++g) {
     if (g >= gend) {
       if (!dyn) break;
-      // the unit is done: publish the unit taken during it, meet, move on
-      if (wave == 0 && lane == 0) uring[(uk + 2) % 3] = ugrab;
-      lds_barrier();
-      ++uk;
-      const uint32_t u = uread(uk % 3);
-      if (u >= nunits) break;
-      const uint32_t un = uread((uk + 1) % 3);
+      uint32_t u, un;
+      if (wdyn) {  // the wave's next unit, and the one taken during this unit after it
+        u = unx;
+        if (u >= nunits) break;
+        un = urd(ugrab);
+        if (lane == 0) ugrab = __hip_atomic_fetch_add(args_ptr()->dyn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        // the unit is done: publish the unit taken during it, meet, move on
+        if (wave == 0 && lane == 0) uring[(uk + 2) % 3] = ugrab;
+        lds_barrier();
+        ++uk;
+        u = uread(uk % 3);
+        if (u >= nunits) break;
+        un = uread((uk + 1) % 3);
+        if (wave == 0 && lane == 0)
+          ugrab = __hip_atomic_fetch_add(args_ptr()->dyn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      unx = un;
       gbeg = u * du;
-      gend = gbeg + du < ng32 ? gbeg + du : ng32;
-      gnext_unit = un < nunits ? un * du : ng32;
-      if (wave == 0 && lane == 0)
-        ugrab = __hip_atomic_fetch_add(args_ptr()->dyn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gend = gbeg + du < npos ? gbeg + du : npos;
+      gnext_unit = un < nunits ? un * du : npos;
       g = gbeg;
     }
-    const uint64_t b = (uint64_t)g * 4 + wave;
+    const uint64_t b = bat(g);
     if (b >= nb) continue;  // the last group's missing batches
     // the wave's next batch (its first frame is prefetched during this batch's last one)
-    const uint64_t bnx = (uint64_t)(g + 1 < gend ? g + 1 : gnext_unit) * 4 + wave;
+    const uint64_t bnx = bat(g + 1 < gend ? g + 1 : gnext_unit);
     const uint64_t f0 = b * FPW;
     // ------------------------------------------------------------- phase 1
     for (int j = 0; j < FPW; ++j) {
@@ -2216,12 +2242,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       prio_lo<4>();
     }
   }
-  if (dyn && threadIdx.x == 0) {
-    // the last workgroup to finish resets the schedule's counters for the stream's next launch (the
-    // release orders this workgroup's last take before its count, so every take precedes the reset)
+  if (dyn && (wdyn ? lane == 0 : threadIdx.x == 0)) {
+    // the last workgroup (wave, dyn_mode 2) to finish resets the schedule's counters for the stream's
+    // next launch (the release orders its last take before its count, so every take precedes the reset)
     uint32_t* const ctr = args_ptr()->dyn;
     (void)ugrab;
-    if (__hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+    if (__hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x * (wdyn ? 4u : 1u) - 1) {
       __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -92,6 +92,8 @@ struct KernelArgs {
   // between launches: the last workgroup, counted in dyn[1], resets both); null: static shares.
   uint32_t* dyn;
   uint32_t dyn_unit;
+  uint32_t dyn_mode;     // 1: a workgroup takes units of dyn_unit groups (a barrier per unit); 2: a wave
+                         // takes units of dyn_unit batches on its own
 };
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.

@@ -457,7 +457,8 @@ struct mgx_plan {
   int chain_groups = 0;  // MGX_FLAG_MFCC_REFERENCE: 8-step groups of the mel chains (chain_schedule)
   int chain_pair = 0;  // ... over two consecutive batches of a wave (8 frames)
   bool dyn_on = true;  // the run-time schedule (KernelArgs::dyn) for large launches
-  int dyn_unit = 2;    // its unit, in groups of 16 frames
+  int dyn_unit = 2;    // its unit: groups of 16 frames (dyn_mode 1) or batches of 4 (dyn_mode 2)
+  int dyn_mode = 1;    // 1: units per workgroup, 2: units per wave
   // Per-stream device scratch, one set per stream a launch used (the launches of one stream run
   // in order, those of two streams may overlap): the scalar windows (kernels.hip scalar_pass) and,
   // for the reference-order MFCC, the mel chains' power rows (mel_chains). Each set's event is
@@ -638,6 +639,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   if (const char* sb = getenv("MGX_SMALL_BATCH_FRAMES")) p->small_max = (uint64_t)std::max(0, atoi(sb));
   if (const char* dv = getenv("MGX_DYN")) p->dyn_on = atoi(dv) != 0;
   if (const char* du = getenv("MGX_DYN_UNIT")) p->dyn_unit = std::max(1, std::min(64, atoi(du)));
+  if (const char* dm = getenv("MGX_DYN_MODE")) p->dyn_mode = atoi(dm) == 2 ? 2 : 1;
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
@@ -802,11 +804,13 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
   // MFCC's kernels (their paired batches run on consecutive batches of a wave) and the small host
   // path's launches (a few frames). $MGX_DYN=0 keeps the static shares; $MGX_DYN_UNIT sets the unit.
   {
-    const uint64_t ng = (nb + 3) / 4;
     const bool chain_launch = a.chain_groups > 0 && a.need_spectrum && a.need_mfcc;
-    if (!chain_launch && !done && p->dyn_on && ng >= (uint64_t)grid * p->dyn_unit * kDynMinUnits && ng < (1ull << 31)) {
+    // (either mode: at least kDynMinUnits units per taker -- 4 dyn_unit batches per workgroup unit,
+    // dyn_unit per wave unit -- is nb >= 4 grid dyn_unit kDynMinUnits)
+    if (!chain_launch && !done && p->dyn_on && nb >= 4ull * grid * p->dyn_unit * kDynMinUnits && nb < (1ull << 31)) {
       a.dyn = ring->dyn;
       a.dyn_unit = (uint32_t)p->dyn_unit;
+      a.dyn_mode = (uint32_t)p->dyn_mode;
     }
   }
   if (a.scal_defer) {

@@ -3,7 +3,7 @@
 run-time units of U groups, KernelArgs::dyn): every plan extracts the same device frames with every
 feature; outputs compared bit for bit against the static plan; then interleaved rounds of 20 launches
 serialised on one stream (the bench's kernel_ms) and 40 launches pipelined over two streams (its period).
-usage: python tools/dyn_ab.py [N ...]   (env DYN_UNITS="1 2 4", ROUNDS=7)"""
+usage: python tools/dyn_ab.py [N ...]   (env DYN="1:2 1:4 2:2" -- mode:unit pairs, ROUNDS=7)"""
 import os
 import sys
 
@@ -14,25 +14,26 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from meyda_amd import capi  # noqa: E402
 
 
-def make_plan(n, dyn, unit):
+def make_plan(n, dyn, unit, mode=1):
     os.environ["MGX_DYN"] = "1" if dyn else "0"
     os.environ["MGX_DYN_UNIT"] = str(unit)
+    os.environ["MGX_DYN_MODE"] = str(mode)
     try:
         return capi.Plan(buffer_size=n)
     finally:
-        del os.environ["MGX_DYN"], os.environ["MGX_DYN_UNIT"]
+        del os.environ["MGX_DYN"], os.environ["MGX_DYN_UNIT"], os.environ["MGX_DYN_MODE"]
 
 
 def main():
     ns = [int(a) for a in sys.argv[1:]] or [1024, 2048, 512]
-    units = [int(u) for u in os.environ.get("DYN_UNITS", "1 2 4").split()]
+    specs = [tuple(int(t) for t in v.split(":")) for v in os.environ.get("DYN", "1:2 1:4 2:1 2:2").split()]
     rounds = int(os.environ.get("ROUNDS", "7"))
     s0, s1 = torch.cuda.current_stream(), torch.cuda.Stream()
     for n in ns:
         F = int(os.environ.get("FRAMES", "262144"))
         x = torch.empty(F, n, dtype=torch.float32, device="cuda")
         capi.synth_frames_device(x, 0x6D657964)
-        variants = [("static", make_plan(n, False, 2))] + [("dyn%d" % u, make_plan(n, True, u)) for u in units]
+        variants = [("static", make_plan(n, False, 2))] + [("m%du%d" % (m, u), make_plan(n, True, u, m)) for m, u in specs]
         feats = capi.ALL_FEATURES
         ref = None
         sets = {}

@@ -5,7 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r5a; mkdir -p $O
 echo "[r5a] dyn A/B"
-DYN_UNITS="2 4 8" timeout -k 10 300 python -u tools/dyn_ab.py 1024 2048 512 > $O/dyn_ab.log 2>&1 || { tail -30 $O/dyn_ab.log; exit 1; }
+DYN="1:2 1:4 2:1 2:2" timeout -k 10 300 python -u tools/dyn_ab.py 1024 2048 512 > $O/dyn_ab.log 2>&1 || { tail -30 $O/dyn_ab.log; exit 1; }
 grep -v amdgpu.ids $O/dyn_ab.log
 echo "[r5a] tests"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 160 --timeout-method thread -p no:cacheprovider > $O/t.log 2>&1 || { tail -40 $O/t.log; exit 1; }
