@@ -1013,39 +1013,66 @@ template <int N, bool PAIR>
 __device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec* recs, float2* buf, bool have_cur) {
   constexpr bool pair = PAIR;
   constexpr int L = N / 2;
+  constexpr int K = chain_k(N);  // chains a lane runs side by side (chain_schedule's streams)
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) f32x4* GF4;
   static_assert(sizeof(FrameRec) == kRecBytes && offsetof(FrameRec, lm) == kRecLmOff, "chain_schedule's record offsets");
   const auto ctl = gbl(q->t.chain_ctl);
   constexpr int F = PAIR ? 8 : 4;
+  constexpr int NL = 64 / F;  // lane groups: group t runs tracks t, t + NL, ... (one per stream)
   const int ng = q->chain_groups;
-  const auto wp = gbl(q->t.chain_w) + (lane / F) * (ng * 8);
   unsigned char* const rb = reinterpret_cast<unsigned char*>(recs);
-  float* const scratch = reinterpret_cast<float*>(buf) + lane;
-  auto store = [&](uint32_t c, double acc) {
-    float* dst = (c & (1u << 26)) ? reinterpret_cast<float*>(rb + ((c >> 13) & 0xFFFu)) : scratch;
+  auto store = [&](int s, uint32_t c, double acc) {
+    // the chain that ends here, or the stream's scratch word in the (free) slot buffer
+    float* dst = (c & (1u << 26)) ? reinterpret_cast<float*>(rb + ((c >> 13) & 0xFFFu))
+                                  : reinterpret_cast<float*>(buf) + lane + 64 * s;
     *dst = (float)acc;
   };
-  double acc = 0.0;  // the Float32Array element, held exactly in double
-  uint32_t c = ctl[lane], cn = ctl[64 + lane];  // (the table has ng + 1 >= 2 rows)
-  for (int g = 0; g < ng; ++g) {
-    double w[8];
+  // The K streams' chains are independent: their steps interleave, so each dependent f64 add and its
+  // two roundings overlap the other streams' instead of waiting on their own latency.
+  double acc[K];    // the Float32Array elements, held exactly in double
+  uint32_t c[K], cn[K];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) w[u] = wp[g * 8 + u];
-    const GF4 pr = (GF4)(ring + (c & 0x1FFFu));      // a multiple of 4 floats (chain_schedule)
-    const f32x4 p0 = pr[0], p1 = pr[1];
-    const uint32_t cnn = ctl[(g + 2 < ng ? g + 2 : ng) * 64 + lane];
-    const float p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-    store(c, acc);  // the chain that ends here (or the scratch word)
-    // a chain starting here adds its first product to 0 (a select: acc may be an overflowed +inf)
-    const double a0 = (c & (1u << 25)) ? 0.0 : acc;
-    acc = (double)(float)(a0 + w[0] * (double)p[0]);
-#pragma unroll
-    for (int u = 1; u < 8; ++u) acc = (double)(float)(acc + w[u] * (double)p[u]);  // two roundings, the float32 store
-    c = cn;
-    cn = cnn;
+  for (int st = 0; st < K; ++st) {
+    acc[st] = 0.0;
+    c[st] = ctl[st * 64 + lane];         // group 0 (the table has ng + 1 >= 2 rows per stream)
+    cn[st] = ctl[(K + st) * 64 + lane];  // group 1
   }
-  store(c, acc);
+  for (int g = 0; g < ng; ++g) {
+    double w[K][8];
+    float p[K][8];
+    uint32_t cnn[K];
+#pragma unroll
+    for (int st = 0; st < K; ++st) {
+      const auto wp = gbl(q->t.chain_w) + ((lane / F) + st * NL) * (ng * 8);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[st][u] = wp[g * 8 + u];
+      const GF4 pr = (GF4)(ring + (c[st] & 0x1FFFu));  // a multiple of 4 floats (chain_schedule)
+      const f32x4 p0 = pr[0], p1 = pr[1];
+      p[st][0] = p0.x; p[st][1] = p0.y; p[st][2] = p0.z; p[st][3] = p0.w;
+      p[st][4] = p1.x; p[st][5] = p1.y; p[st][6] = p1.z; p[st][7] = p1.w;
+      cnn[st] = ctl[((g + 2 < ng ? g + 2 : ng) * K + st) * 64 + lane];
+    }
+#pragma unroll
+    for (int st = 0; st < K; ++st) {
+      store(st, c[st], acc[st]);
+      // a chain starting here adds its first product to 0 (a select: acc may be an overflowed +inf)
+      const double a0 = (c[st] & (1u << 25)) ? 0.0 : acc[st];
+      acc[st] = (double)(float)(a0 + w[st][0] * (double)p[st][0]);
+    }
+#pragma unroll
+    for (int u = 1; u < 8; ++u)
+#pragma unroll
+      for (int st = 0; st < K; ++st)
+        acc[st] = (double)(float)(acc[st] + w[st][u] * (double)p[st][u]);  // two roundings, the float32 store
+#pragma unroll
+    for (int st = 0; st < K; ++st) {
+      c[st] = cn[st];
+      cn[st] = cnn[st];
+    }
+  }
+#pragma unroll
+  for (int st = 0; st < K; ++st) store(st, c[st], acc[st]);
   // the non-finite frames' own sums back from their ring slots (wave-uniform, rare)
   wave_sync();
   for (int fr = 0; fr < F; ++fr) {
@@ -1668,12 +1695,13 @@ __device__ __forceinline__ double scalar_value(KArgs* q, const Rec& rc, int sc) 
 }
 
 // The scalar features of one window of a wave's batches (kScalDefer), one lane per frame: lane l
-// takes frame l & 3 of the window's batch l >> 2 (nbat batches), its ScalIn and its frame index from
-// the wave's window in device memory (win: word c of lane l at c * 64 + l, phase 2 put them there),
-// and stores every requested feature -- the formulas of scalar_value, evaluated
+// takes frame l & 3 of the window's batch l >> 2 (nbat batches; frame f0 + (l >> 2) fstep + (l & 3)),
+// its ScalIn from the wave's window in device memory (win: word c of lane l at c * 64 + l, phase 2
+// put it there), and stores every requested feature -- the formulas of scalar_value, evaluated
 // with each feature a constant, so the thirteen share their common terms and nothing diverges.
 template <int N, bool SUB, class WinPtr>
-__device__ __forceinline__ void scalar_pass(KArgs* q, WinPtr win, void* const* kptr, int nbat, int lane) {
+__device__ __forceinline__ void scalar_pass(KArgs* q, WinPtr win, void* const* kptr, uint64_t f0, uint64_t fstep, int nbat,
+                                            int lane) {
   // the window's words were stored by this wave (phase 2 of each batch): visible to its loads
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -1683,9 +1711,8 @@ __device__ __forceinline__ void scalar_pass(KArgs* q, WinPtr win, void* const* k
   for (int c = 0; c < 10; ++c) wd[c] = w[c * 64];
   ScalIn r;
   __builtin_memcpy(&r, wd, sizeof(r));
-  const bool ok0 = (lane >> 2) < nbat;
-  const uint64_t f = ok0 ? (uint64_t)w[10 * 64] : 0;  // word 10: the frame's index (phase 2 put it there)
-  const bool ok = ok0 && f < q->num_frames;
+  const uint64_t f = f0 + (uint64_t)(lane >> 2) * fstep + (uint64_t)(lane & 3);
+  const bool ok = (lane >> 2) < nbat && f < q->num_frames;
   double v[MGX_NUM_SCALARS];
 #pragma unroll
   for (int sc = 0; sc < MGX_NUM_SCALARS; ++sc) v[sc] = scalar_value<N, SUB>(q, r, sc);
@@ -1851,26 +1878,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     const GTwf src = gbl(ap->t.twf);
     for (int i = threadIdx.x; i < TwLdsF<N>::count; i += kThreads) d[i] = ld_twf(src, TwLdsF<N>::first + i);
   }
-  // the run-time schedule's ring of unit indices (KernelArgs::dyn; words 26..28 of the limits table)
-  uint32_t* const uring = reinterpret_cast<uint32_t*>(smem + LY::kc_off + 16 * 8) + 26;
-  uint32_t pu0 = 0, pu1 = 0;  // dyn_mode 2: this wave's first two units (lane 0)
-  if (!CHAIN && ap->dyn) {
-    // the first two units (later ones are taken two ahead: the next unit's first frame is prefetched
-    // during the current unit's last one) -- the workgroup's (dyn_mode 1, into the LDS ring) or the
-    // wave's (dyn_mode 2). Vector atomics at device scope: the counter is shared by every XCD.
-    uint32_t* const ctr = ap->dyn;
-    if (ap->dyn_mode == 2) {
-      if (lane == 0) {
-        pu0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pu1 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else if (threadIdx.x == 0) {
-      const uint32_t u0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t u1 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uring[0] = u0;
-      uring[1] = u1;
-    }
-  }
   if (ap->need_spectrum && ap->need_mfcc) {
     const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
     const auto dct = gbl(ap->t.dct);
@@ -1955,41 +1962,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     g0 = g0 < ng ? g0 : ng;
     g1 = g0 + per < ng ? g0 + per : ng;
   }
-  // The run-time schedule (KernelArgs::dyn): instead of a fixed share, each workgroup takes units of
-  // dyn_unit consecutive groups from a device-wide counter, two ahead, and its four waves meet at a
-  // workgroup barrier after each unit (where the next unit's index is published in LDS). The waves of
-  // the four workgroups of a CU progress at different rates (the arbiter favours the oldest wave) and
-  // so do the XCDs: with static shares the launch's waves ended between 501 and 608 us
-  // (profiles/r04_wave_times.txt); units dealt at run time end within about a unit of each other.
-  // (group indices as 32-bit values: a launch holds fewer than 2^32 groups of 16 frames -- plan.cpp
-  // takes this schedule only below that -- and the SGPRs are scarce at N = 2048)
-  // dyn_mode 2: units of dyn_unit batches taken by each wave on its own (no barrier; the units of
-  // a wave's neighbours may run on other XCDs, so output lines can be written in pieces).
-  // Positions: groups (static, dyn_mode 1: the wave's batch of group p is 4 p + wave) or batches.
-  const bool dyn = !CHAIN && args_ptr()->dyn != nullptr;  // (never with the paired-batch chains)
-  const bool wdyn = dyn && args_ptr()->dyn_mode == 2;
-  const uint32_t du = dyn ? args_ptr()->dyn_unit : 1u;
-  const uint32_t ng32 = (uint32_t)ng;
-  const uint32_t npos = wdyn ? (uint32_t)nb : ng32;
-  const uint32_t nunits = dyn ? (npos + du - 1) / du : 0;
-  uint32_t uk = 0;      // units this workgroup has run
-  uint32_t ugrab = 0;   // lane 0 of wave 0 (of every wave with dyn_mode 2): the unit taken two ahead
-  uint32_t unx = 0;     // dyn_mode 2: the wave's next unit
-  uint32_t gbeg = (uint32_t)g0, gend = (uint32_t)g1, gnext_unit = (uint32_t)g1;  // this unit's positions; the next unit's first
-  // (unit indices read from LDS are made wave-uniform: the schedule's state then lives in SGPRs)
-  auto uread = [&](int i) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)uring[i]); };
-  auto urd = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
-  if (dyn) {
-    const uint32_t u = wdyn ? urd(pu0) : uread(0), un = wdyn ? urd(pu1) : uread(1);
-    gbeg = u * du;
-    gend = u < nunits ? (gbeg + du < npos ? gbeg + du : npos) : gbeg;
-    gnext_unit = un < nunits ? un * du : npos;
-    unx = un;
-    if ((wdyn ? lane == 0 : (wave == 0 && lane == 0)) && u < nunits)
-      ugrab = __hip_atomic_fetch_add(args_ptr()->dyn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  auto bat = [&](uint32_t p) -> uint64_t { return wdyn ? (uint64_t)p : (uint64_t)p * 4 + wave; };
-  const uint64_t b0 = bat(gbeg);
+  const uint64_t b0 = g0 * 4 + wave, bend = g1 * 4 < nb ? g1 * 4 : nb;
   // Loads are unconditional (the frame index is clamped; results of frames past the end
   // are never stored), so they issue back to back with no branches or waits between them.
   // With G::PREFETCH the next frame of the wave is loaded while this one is processed.
@@ -2022,38 +1995,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   if constexpr (G::PREFETCH) load(xn, b0, 0);
 
   int it = 0;  // the wave's batch count (CHAIN with paired batches: the pair's second when odd)
-  // (static: the groups [g0, g1); run-time: unit after unit, a barrier between them. A wave whose batch
-  // of the last, partial group is past the end skips it, and still meets the barriers.)
-  for (uint32_t g = gbeg;; ++g) {
-    if (g >= gend) {
-      if (!dyn) break;
-      uint32_t u, un;
-      if (wdyn) {  // the wave's next unit, and the one taken during this unit after it
-        u = unx;
-        if (u >= nunits) break;
-        un = urd(ugrab);
-        if (lane == 0) ugrab = __hip_atomic_fetch_add(args_ptr()->dyn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        // the unit is done: publish the unit taken during it, meet, move on
-        if (wave == 0 && lane == 0) uring[(uk + 2) % 3] = ugrab;
-        lds_barrier();
-        ++uk;
-        u = uread(uk % 3);
-        if (u >= nunits) break;
-        un = uread((uk + 1) % 3);
-        if (wave == 0 && lane == 0)
-          ugrab = __hip_atomic_fetch_add(args_ptr()->dyn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      unx = un;
-      gbeg = u * du;
-      gend = gbeg + du < npos ? gbeg + du : npos;
-      gnext_unit = un < nunits ? un * du : npos;
-      g = gbeg;
-    }
-    const uint64_t b = bat(g);
-    if (b >= nb) continue;  // the last group's missing batches
-    // the wave's next batch (its first frame is prefetched during this batch's last one)
-    const uint64_t bnx = bat(g + 1 < gend ? g + 1 : gnext_unit);
+  for (uint64_t b = b0; b < bend; b += wstride, ++it) {
     const uint64_t f0 = b * FPW;
     // ------------------------------------------------------------- phase 1
     for (int j = 0; j < FPW; ++j) {
@@ -2068,11 +2010,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
 #pragma unroll
         for (int c = 0; c < CH; ++c) x[c] = xn[c];
         if (j + 1 < FPW) load(xn, b, j + 1);
-        else load(xn, bnx, 0);
+        else load(xn, b + wstride, 0);
       } else if constexpr (G::PF == 2) {
 #pragma unroll
         for (int c = 0; c < CH; ++c) x[c] = xn[c];
-        next = frame_ptr(j + 1 < FPW ? b : bnx, j + 1 < FPW ? j + 1 : 0);
+        next = frame_ptr(j + 1 < FPW ? b : b + wstride, j + 1 < FPW ? j + 1 : 0);
       } else {
         load(x, b, j);
       }
@@ -2174,9 +2116,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
           const unsigned off = 8u * (unsigned)c + (c >= 8 ? 440u : 0u);  // words 0..7, then 63..64
           const uint64_t wv = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const unsigned char*>(&rec_at(recs, fb)) + off);
           win[__umul24((unsigned)c, 64u) + (unsigned)(4 * slot + fb)] = wv;
-        } else if (l2 < 11 * FPW) {  // word 10: the frame's index (the run-time schedule deals batches anywhere)
-          const int fb = l2 - 10 * FPW;
-          win[10u * 64u + (unsigned)(4 * slot + fb)] = f0 + (uint64_t)fb;
         }
       }
       // the scalar features: one lane per (feature, frame); the loudness total, perceptual
@@ -2201,7 +2140,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     // outputs identical (profiles/r03_group_sync.txt). Every wave has a batch in a full group, so
     // all four reach the same barriers. N = 512 and 2048 lost 1.6 % and 2.3 % and keep none.
     if constexpr (G::GROUP_SYNC > 0) {
-      if (!dyn && (uint64_t)g * 4 + 3 < nb && g % G::GROUP_SYNC == G::GROUP_SYNC - 1) __builtin_amdgcn_s_barrier();
+      const uint64_t g = (b - wave) / 4;
+      if (g * 4 + 3 < nb && g % G::GROUP_SYNC == G::GROUP_SYNC - 1) __builtin_amdgcn_s_barrier();
     }
     // A full scalar window: its pass right after the group barrier (a window ends on an odd group,
     // where the barrier is), so the workgroup's four waves write their 16-byte pieces of each
@@ -2211,11 +2151,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       if (q->scal_defer) {
         prio_hi<4>();
         scalar_pass<N, SUB>(q, uniform_ptr(gbl(q->scal_rows) + ((uint64_t)blockIdx.x * 4 + wave) * (uint64_t)kScalWords),
-                            reinterpret_cast<void* const*>(smem + LY::kc_off), kScalBatches, opaque(lane));
+                            reinterpret_cast<void* const*>(smem + LY::kc_off),
+                            (b - (uint64_t)(kScalBatches - 1) * wstride) * FPW, wstride * FPW, kScalBatches, opaque(lane));
         prio_lo<4>();
       }
     }
-    ++it;
   }
   if (kScalDefer && args_ptr()->scal_defer && (it & (kScalBatches - 1)) != 0) {
     // the wave's last window, with fewer than kScalBatches batches
@@ -2223,7 +2163,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     const int nbat = it & (kScalBatches - 1), l2 = opaque(lane);
     prio_hi<4>();
     scalar_pass<N, SUB>(q, uniform_ptr(gbl(q->scal_rows) + ((uint64_t)blockIdx.x * 4 + wave) * (uint64_t)kScalWords),
-                        reinterpret_cast<void* const*>(smem + LY::kc_off), nbat, l2);
+                        reinterpret_cast<void* const*>(smem + LY::kc_off), (b0 + (uint64_t)(it - nbat) * wstride) * FPW,
+                        wstride * FPW, nbat, l2);
     prio_lo<4>();
   }
   if constexpr (CHAIN) {
@@ -2240,16 +2181,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       wave_sync();
       mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 32, (b0 + (uint64_t)(it - 1) * wstride) * FPW);
       prio_lo<4>();
-    }
-  }
-  if (dyn && (wdyn ? lane == 0 : threadIdx.x == 0)) {
-    // the last workgroup (wave, dyn_mode 2) to finish resets the schedule's counters for the stream's
-    // next launch (the release orders its last take before its count, so every take precedes the reset)
-    uint32_t* const ctr = args_ptr()->dyn;
-    (void)ugrab;
-    if (__hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x * (wdyn ? 4u : 1u) - 1) {
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (args_ptr()->done_flag) done_signal(args_ptr(), opaque(lane));

@@ -10,15 +10,15 @@ namespace mgx {
 constexpr int kMaxMel = 64;
 // The scalar features run once per window of kScalBatches batches of a wave (kernels.hip
 // scalar_pass), one lane per frame: the window's per-frame inputs (10 8-byte words each, the
-// record's S[0..4], ln2sum, energy, loudness total, zcr | roll_m, loud_max | sharp_sum) and the
-// frame's index (word 10) wait in device memory, kScalWords words per wave.
+// record's S[0..4], ln2sum, energy, loudness total, zcr | roll_m, loud_max | sharp_sum) wait in
+// device memory, kScalWords words per wave.
 #ifndef MGX_SCAL_BATCHES
 #define MGX_SCAL_BATCHES 16
 #endif
 constexpr int kScalBatches = MGX_SCAL_BATCHES;
 // word c of the window's frame l (l = 4 batch + frame, < 4 kScalBatches) at c * 64 + l
 static_assert(4 * kScalBatches <= 64, "a window's frames are lanes of one wave");
-constexpr int kScalWords = 11 * 64;
+constexpr int kScalWords = 10 * 64;
 constexpr int kBark = 24;
 constexpr int kMaxCoeffs = 32;
 constexpr int kThreads = 256;  // 4 waves per workgroup
@@ -28,6 +28,14 @@ constexpr int kRecBytes = 520;  // sizeof(FrameRec) (kernels.hip)
 constexpr int kRecLmOff = 248;  // offsetof(FrameRec, lm)
 constexpr int kChainPairMaxMel = 31;  // paired batches keep two halves of FrameRec::lm (flag at 31)
 constexpr int kChainMaxN = 2048;
+// Chains a lane runs side by side (kernels.hip mel_chains, plan.cpp chain_schedule): each lane group
+// of F lanes runs chain_k(N) tracks, interleaving their steps so one chain's dependent adds overlap the
+// others' latency. (N <= 512 keeps one: its kernels run 5-6 waves per SIMD, whose registers a second
+// stream's weights and rows would overflow.)
+#ifndef MGX_CHAIN_K
+#define MGX_CHAIN_K 2
+#endif
+__host__ __device__ constexpr int chain_k(int n) { return n >= 1024 ? MGX_CHAIN_K : 1; }
 constexpr int kChainSkip = 1 << 30;  // FrameRec.zcr flag bit: a non-finite frame keeps its phase-1 mel sums
 // dwords of one lane's mel record for R bins per lane (R weights, R slot bytes, R keep bytes,
 // 8 bytes of scan keeps and slots), padded to whole 16-byte loads
@@ -87,13 +95,6 @@ struct KernelArgs {
   int chain_pair;        // the chains of two consecutive batches of a wave run together (8 frames, nfilt <= 31)
   float* chain_rows;     // the chains' power rows: 2 FPW x N/2 floats per wave of the grid (kernels.hip mel_chains)
   uint64_t* scal_rows;   // the scalar window: kScalWords 8-byte words per wave of the grid (kernels.hip scalar_pass)
-  // Run-time schedule (kernels.hip extract_kernel): the batch's groups of 16 frames are dealt in
-  // units of dyn_unit groups from the counter dyn[0] (device memory of the launch's stream, zero
-  // between launches: the last workgroup, counted in dyn[1], resets both); null: static shares.
-  uint32_t* dyn;
-  uint32_t dyn_unit;
-  uint32_t dyn_mode;     // 1: a workgroup takes units of dyn_unit groups (a barrier per unit); 2: a wave
-                         // takes units of dyn_unit batches on its own
 };
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.

@@ -54,8 +54,6 @@ const uint64_t kSmallBatchFrames = 512;
 // How long the small path spins on its completion word before it blocks on the stream (a
 // 512-frame batch takes ~0.1 ms; a longer wait is a busy device, where blocking frees the core).
 const int kSmallSpinUs = 2000;
-// A launch takes the run-time schedule when its workgroups get at least this many units each.
-const uint64_t kDynMinUnits = 2;
 const double kJsPi = 3.141592653589793;        // Math.PI
 const double kJsSqrt1_2 = 0.7071067811865476;  // Math.SQRT1_2
 
@@ -338,16 +336,17 @@ void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& 
 // or earlier if it would run past N/2, with leading zero weights (a zero weight times a finite
 // power adds +0); a band without bins (low bands of many-band plans) has one group of zero
 // weights, so its energy is the reference's 0.
-// Packed tracks: the 64 lanes are 64 / F tracks x the F frames (lane = track * F + frame). The
-// bands are dealt to the tracks longest first, each to the least loaded track, and a track runs its
+// Packed tracks: the 64 lanes are 64 / F lane groups x the F frames (lane = group * F + frame), and
+// each lane group runs chain_k(N) tracks side by side (track t on group t % (64 / F), stream t / (64 / F)).
+// The bands are dealt to the tracks longest first, each to the least loaded track, and a track runs its
 // bands' chains back to back, so the lanes stay busy for ngroups = the largest track load (N = 1024,
-// 26 bands: 18 groups instead of the 24 of phases whose length is the phase's longest chain).
-//   ctl[g * 64 + lane], g < ngroups (the lane's row and what happens at the group's start):
+// 26 bands, one stream: 18 groups instead of the 24 of phases whose length is the phase's longest chain).
+//   ctl[(g * chain_k(N) + stream) * 64 + lane], g < ngroups (the row and what happens at the group's start):
 //     bits 0-12 the row offset in floats (frame * L + bin), bit 25 a chain starts here (its first
 //     step adds to 0), bit 26 the finished chain before it is
 //     stored at bits 13-24 (a byte offset into the wave's frame records: FrameRec::lm of its frame
 //     and band); without bit 26 the store goes to the lane's scratch word.
-//   ctl[ngroups * 64 + lane]: the store of the lane's last chain (bit 26 and bits 13-24 only).
+//   ctl[(ngroups * chain_k(N) + stream) * 64 + lane]: the store of the stream's last chain (bit 26, bits 13-24).
 //   w[track * ngroups * 8 + s]: the weight of the track's step s (0 past its last chain).
 struct ChainSched {
   int ngroups = 0;
@@ -358,7 +357,9 @@ struct ChainSched {
 static_assert(8 * (mgx::kChainMaxN / 2) - 1 <= 0x1FFF, "row offsets fit bits 0-12");
 static_assert(3 * mgx::kRecBytes + mgx::kRecLmOff + 4 * (mgx::kMaxMel - 1) <= 0xFFF, "record offsets fit bits 13-24");
 void chain_schedule(const int32_t* b, int nf, int L, int F, ChainSched& cs) {
-  const int ntr = 64 / F;
+  // lane group t (lanes t F .. t F + F - 1) runs tracks t, t + nl, ..., one per stream, side by side
+  const int K = mgx::chain_k(2 * L);
+  const int nl = 64 / F, ntr = nl * K;
   std::vector<int> lo(nf), len(nf), order;
   for (int j = 0; j < nf; ++j) {
     const int first = std::min<int>(b[j], L), end = std::min<int>(b[j + 2], L);
@@ -379,7 +380,7 @@ void chain_schedule(const int32_t* b, int nf, int L, int F, ChainSched& cs) {
   }
   const int ng = *std::max_element(load.begin(), load.end()) / 8;
   cs.ngroups = ng;
-  cs.ctl.assign((size_t)(ng + 1) * 64, 0u);
+  cs.ctl.assign((size_t)(ng + 1) * K * 64, 0u);
   cs.w.assign((size_t)ntr * ng * 8, 0.0);
   auto target = [&](int j, int f) {  // byte offset of FrameRec::lm[band (+32: a pair's first batch)]
     const int lmo = (F == 8 && f < 4) ? 32 : 0;
@@ -398,20 +399,20 @@ void chain_schedule(const int32_t* b, int nf, int L, int F, ChainSched& cs) {
         w[g0 * 8 + s] = v;
       }
       for (int f = 0; f < F; ++f) {
-        const int lane = t * F + f;
+        const int lane = (t % nl) * F + f, st = t / nl;
         for (int g = g0; g < g0 + len[j] / 8; ++g) {
           uint32_t c32 = (uint32_t)(f * L + lo[j] + 8 * (g - g0));
           if (g == g0) c32 |= 1u << 25 | (c > 0 ? target(track[t][c - 1], f) : 0u);
-          cs.ctl[(size_t)g * 64 + lane] = c32;
+          cs.ctl[((size_t)g * K + st) * 64 + lane] = c32;
         }
       }
       g0 += len[j] / 8;
     }
     for (int f = 0; f < F; ++f) {
-      const int lane = t * F + f;
+      const int lane = (t % nl) * F + f, st = t / nl;
       // past the track's last chain: bin 0 of the frame with zero weights (adds +0); no reset
-      for (int g = g0; g < ng; ++g) cs.ctl[(size_t)g * 64 + lane] = (uint32_t)(f * L);
-      cs.ctl[(size_t)ng * 64 + lane] = track[t].empty() ? 0u : target(track[t].back(), f);
+      for (int g = g0; g < ng; ++g) cs.ctl[((size_t)g * K + st) * 64 + lane] = (uint32_t)(f * L);
+      cs.ctl[((size_t)ng * K + st) * 64 + lane] = track[t].empty() ? 0u : target(track[t].back(), f);
     }
   }
 }
@@ -456,9 +457,6 @@ struct mgx_plan {
   int cus = 0;  // compute units of the plan's device
   int chain_groups = 0;  // MGX_FLAG_MFCC_REFERENCE: 8-step groups of the mel chains (chain_schedule)
   int chain_pair = 0;  // ... over two consecutive batches of a wave (8 frames)
-  bool dyn_on = true;  // the run-time schedule (KernelArgs::dyn) for large launches
-  int dyn_unit = 2;    // its unit: groups of 16 frames (dyn_mode 1) or batches of 4 (dyn_mode 2)
-  int dyn_mode = 1;    // 1: units per workgroup, 2: units per wave
   // Per-stream device scratch, one set per stream a launch used (the launches of one stream run
   // in order, those of two streams may overlap): the scalar windows (kernels.hip scalar_pass) and,
   // for the reference-order MFCC, the mel chains' power rows (mel_chains). Each set's event is
@@ -469,7 +467,6 @@ struct mgx_plan {
     uint64_t* scal;
     float* rows;  // null until a reference-order MFCC launch on the stream
     hipEvent_t done;
-    uint32_t* dyn;  // the run-time schedule's two counters (KernelArgs::dyn), zero between launches
   };
   std::vector<ChainRing> chain_rings;
   // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
@@ -637,9 +634,6 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
     else if (atoi(gc) > 0) p->grid_cap = atoi(gc);
   }
   if (const char* sb = getenv("MGX_SMALL_BATCH_FRAMES")) p->small_max = (uint64_t)std::max(0, atoi(sb));
-  if (const char* dv = getenv("MGX_DYN")) p->dyn_on = atoi(dv) != 0;
-  if (const char* du = getenv("MGX_DYN_UNIT")) p->dyn_unit = std::max(1, std::min(64, atoi(du)));
-  if (const char* dm = getenv("MGX_DYN_MODE")) p->dyn_mode = atoi(dm) == 2 ? 2 : 1;
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
@@ -693,7 +687,6 @@ int mgx_plan_destroy(mgx_plan* p) {
   for (auto& r : p->chain_rings) {
     (void)hipEventDestroy(r.done);
     if (r.scal) (void)hipFree(r.scal);
-    if (r.dyn) (void)hipFree(r.dyn);
     if (r.rows) (void)hipFree(r.rows);
   }
   for (int i = 0; i < 2; ++i) {
@@ -788,30 +781,8 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
     hipEvent_t done = nullptr;
     e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
     if (e != hipSuccess) return hip_fail(e, "hipEventCreate(stream scratch)");
-    uint32_t* dyn = nullptr;
-    e = hipMalloc(reinterpret_cast<void**>(&dyn), 2 * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemsetAsync(dyn, 0, 2 * sizeof(uint32_t), (hipStream_t)stream);
-    if (e != hipSuccess) {
-      if (dyn) (void)hipFree(dyn);
-      (void)hipEventDestroy(done);
-      return hip_fail(e, "schedule counters");
-    }
-    p->chain_rings.push_back({stream, nullptr, nullptr, done, dyn});
+    p->chain_rings.push_back({stream, nullptr, nullptr, done});
     ring = &p->chain_rings.back();
-  }
-  // The run-time schedule (kernels.hip: units of dyn_unit groups of 16 frames from a device-wide
-  // counter) for launches with at least kDynMinUnits units per workgroup, except the reference-order
-  // MFCC's kernels (their paired batches run on consecutive batches of a wave) and the small host
-  // path's launches (a few frames). $MGX_DYN=0 keeps the static shares; $MGX_DYN_UNIT sets the unit.
-  {
-    const bool chain_launch = a.chain_groups > 0 && a.need_spectrum && a.need_mfcc;
-    // (either mode: at least kDynMinUnits units per taker -- 4 dyn_unit batches per workgroup unit,
-    // dyn_unit per wave unit -- is nb >= 4 grid dyn_unit kDynMinUnits)
-    if (!chain_launch && !done && p->dyn_on && nb >= 4ull * grid * p->dyn_unit * kDynMinUnits && nb < (1ull << 31)) {
-      a.dyn = ring->dyn;
-      a.dyn_unit = (uint32_t)p->dyn_unit;
-      a.dyn_mode = (uint32_t)p->dyn_mode;
-    }
   }
   if (a.scal_defer) {
     // kScalWords words for each wave of the largest grid (4 waves per workgroup), allocated by the

@@ -50,23 +50,6 @@ PATCHES = {
     "chain_none": [("        if (q->chain_pair) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);",
                     "        if (opaque(0)) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);")],
     # the chains' weight and row loads replaced by values from the control word (no loads)
-    "chain_noload": [("""#pragma unroll
-    for (int u = 0; u < 8; ++u) w[u] = wp[g * 8 + u];
-    const GF4 pr = (GF4)(ring + (c & 0x1FFFu));      // a multiple of 4 floats (chain_schedule)
-    const f32x4 p0 = pr[0], p1 = pr[1];""",
-                      """#pragma unroll
-    for (int u = 0; u < 8; ++u) w[u] = (double)(int)((c >> u) & 7u) * 0.125;
-    const f32x4 p0 = {(float)(c & 255u), (float)((c >> 3) & 255u), (float)((c >> 5) & 255u), (float)((c >> 7) & 255u)};
-    const f32x4 p1 = p0 * 0.5f;""")],
-    # the 8 steps of a chain group independent (summed by a tree): the dependency latency's share
-    "chain_nodep": [("""    acc = (double)(float)(a0 + w[0] * (double)p[0]);
-#pragma unroll
-    for (int u = 1; u < 8; ++u) acc = (double)(float)(acc + w[u] * (double)p[u]);  // two roundings, the float32 store""",
-                     """    double t[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) t[u] = (double)(float)((u ? (double)u : a0) + w[u] * (double)p[u]);
-    acc = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));""")],
-    # the CHAIN kernels' power-row stores to the device-memory ring skipped (the chains read stale rows)
     "chain_norows": [("      for (int jj = 0; jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];",
                       "      for (int jj = 0; opaque(0) && jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];")],
     # the fence before the chains (a vmcnt(0) wait: the next frame's prefetch, the row stores) dropped
