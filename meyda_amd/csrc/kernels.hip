@@ -1013,66 +1013,39 @@ template <int N, bool PAIR>
 __device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec* recs, float2* buf, bool have_cur) {
   constexpr bool pair = PAIR;
   constexpr int L = N / 2;
-  constexpr int K = chain_k(N);  // chains a lane runs side by side (chain_schedule's streams)
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) f32x4* GF4;
   static_assert(sizeof(FrameRec) == kRecBytes && offsetof(FrameRec, lm) == kRecLmOff, "chain_schedule's record offsets");
   const auto ctl = gbl(q->t.chain_ctl);
   constexpr int F = PAIR ? 8 : 4;
-  constexpr int NL = 64 / F;  // lane groups: group t runs tracks t, t + NL, ... (one per stream)
   const int ng = q->chain_groups;
+  const auto wp = gbl(q->t.chain_w) + (lane / F) * (ng * 8);
   unsigned char* const rb = reinterpret_cast<unsigned char*>(recs);
-  auto store = [&](int s, uint32_t c, double acc) {
-    // the chain that ends here, or the stream's scratch word in the (free) slot buffer
-    float* dst = (c & (1u << 26)) ? reinterpret_cast<float*>(rb + ((c >> 13) & 0xFFFu))
-                                  : reinterpret_cast<float*>(buf) + lane + 64 * s;
+  float* const scratch = reinterpret_cast<float*>(buf) + lane;
+  auto store = [&](uint32_t c, double acc) {
+    float* dst = (c & (1u << 26)) ? reinterpret_cast<float*>(rb + ((c >> 13) & 0xFFFu)) : scratch;
     *dst = (float)acc;
   };
-  // The K streams' chains are independent: their steps interleave, so each dependent f64 add and its
-  // two roundings overlap the other streams' instead of waiting on their own latency.
-  double acc[K];    // the Float32Array elements, held exactly in double
-  uint32_t c[K], cn[K];
-#pragma unroll
-  for (int st = 0; st < K; ++st) {
-    acc[st] = 0.0;
-    c[st] = ctl[st * 64 + lane];         // group 0 (the table has ng + 1 >= 2 rows per stream)
-    cn[st] = ctl[(K + st) * 64 + lane];  // group 1
-  }
+  double acc = 0.0;  // the Float32Array element, held exactly in double
+  uint32_t c = ctl[lane], cn = ctl[64 + lane];  // (the table has ng + 1 >= 2 rows)
   for (int g = 0; g < ng; ++g) {
-    double w[K][8];
-    float p[K][8];
-    uint32_t cnn[K];
+    double w[8];
 #pragma unroll
-    for (int st = 0; st < K; ++st) {
-      const auto wp = gbl(q->t.chain_w) + ((lane / F) + st * NL) * (ng * 8);
+    for (int u = 0; u < 8; ++u) w[u] = wp[g * 8 + u];
+    const GF4 pr = (GF4)(ring + (c & 0x1FFFu));      // a multiple of 4 floats (chain_schedule)
+    const f32x4 p0 = pr[0], p1 = pr[1];
+    const uint32_t cnn = ctl[(g + 2 < ng ? g + 2 : ng) * 64 + lane];
+    const float p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+    store(c, acc);  // the chain that ends here (or the scratch word)
+    // a chain starting here adds its first product to 0 (a select: acc may be an overflowed +inf)
+    const double a0 = (c & (1u << 25)) ? 0.0 : acc;
+    acc = (double)(float)(a0 + w[0] * (double)p[0]);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) w[st][u] = wp[g * 8 + u];
-      const GF4 pr = (GF4)(ring + (c[st] & 0x1FFFu));  // a multiple of 4 floats (chain_schedule)
-      const f32x4 p0 = pr[0], p1 = pr[1];
-      p[st][0] = p0.x; p[st][1] = p0.y; p[st][2] = p0.z; p[st][3] = p0.w;
-      p[st][4] = p1.x; p[st][5] = p1.y; p[st][6] = p1.z; p[st][7] = p1.w;
-      cnn[st] = ctl[((g + 2 < ng ? g + 2 : ng) * K + st) * 64 + lane];
-    }
-#pragma unroll
-    for (int st = 0; st < K; ++st) {
-      store(st, c[st], acc[st]);
-      // a chain starting here adds its first product to 0 (a select: acc may be an overflowed +inf)
-      const double a0 = (c[st] & (1u << 25)) ? 0.0 : acc[st];
-      acc[st] = (double)(float)(a0 + w[st][0] * (double)p[st][0]);
-    }
-#pragma unroll
-    for (int u = 1; u < 8; ++u)
-#pragma unroll
-      for (int st = 0; st < K; ++st)
-        acc[st] = (double)(float)(acc[st] + w[st][u] * (double)p[st][u]);  // two roundings, the float32 store
-#pragma unroll
-    for (int st = 0; st < K; ++st) {
-      c[st] = cn[st];
-      cn[st] = cnn[st];
-    }
+    for (int u = 1; u < 8; ++u) acc = (double)(float)(acc + w[u] * (double)p[u]);  // two roundings, the float32 store
+    c = cn;
+    cn = cnn;
   }
-#pragma unroll
-  for (int st = 0; st < K; ++st) store(st, c[st], acc[st]);
+  store(c, acc);
   // the non-finite frames' own sums back from their ring slots (wave-uniform, rare)
   wave_sync();
   for (int fr = 0; fr < F; ++fr) {

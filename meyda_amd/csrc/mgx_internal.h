@@ -28,14 +28,6 @@ constexpr int kRecBytes = 520;  // sizeof(FrameRec) (kernels.hip)
 constexpr int kRecLmOff = 248;  // offsetof(FrameRec, lm)
 constexpr int kChainPairMaxMel = 31;  // paired batches keep two halves of FrameRec::lm (flag at 31)
 constexpr int kChainMaxN = 2048;
-// Chains a lane runs side by side (kernels.hip mel_chains, plan.cpp chain_schedule): each lane group
-// of F lanes runs chain_k(N) tracks, interleaving their steps so one chain's dependent adds overlap the
-// others' latency. (N <= 512 keeps one: its kernels run 5-6 waves per SIMD, whose registers a second
-// stream's weights and rows would overflow.)
-#ifndef MGX_CHAIN_K
-#define MGX_CHAIN_K 2
-#endif
-__host__ __device__ constexpr int chain_k(int n) { return n >= 1024 ? MGX_CHAIN_K : 1; }
 constexpr int kChainSkip = 1 << 30;  // FrameRec.zcr flag bit: a non-finite frame keeps its phase-1 mel sums
 // dwords of one lane's mel record for R bins per lane (R weights, R slot bytes, R keep bytes,
 // 8 bytes of scan keeps and slots), padded to whole 16-byte loads

@@ -336,17 +336,16 @@ void mel_lane_tables(const std::vector<uint8_t>& seg, const std::vector<float>& 
 // or earlier if it would run past N/2, with leading zero weights (a zero weight times a finite
 // power adds +0); a band without bins (low bands of many-band plans) has one group of zero
 // weights, so its energy is the reference's 0.
-// Packed tracks: the 64 lanes are 64 / F lane groups x the F frames (lane = group * F + frame), and
-// each lane group runs chain_k(N) tracks side by side (track t on group t % (64 / F), stream t / (64 / F)).
-// The bands are dealt to the tracks longest first, each to the least loaded track, and a track runs its
+// Packed tracks: the 64 lanes are 64 / F tracks x the F frames (lane = track * F + frame). The
+// bands are dealt to the tracks longest first, each to the least loaded track, and a track runs its
 // bands' chains back to back, so the lanes stay busy for ngroups = the largest track load (N = 1024,
-// 26 bands, one stream: 18 groups instead of the 24 of phases whose length is the phase's longest chain).
-//   ctl[(g * chain_k(N) + stream) * 64 + lane], g < ngroups (the row and what happens at the group's start):
+// 26 bands: 18 groups instead of the 24 of phases whose length is the phase's longest chain).
+//   ctl[g * 64 + lane], g < ngroups (the lane's row and what happens at the group's start):
 //     bits 0-12 the row offset in floats (frame * L + bin), bit 25 a chain starts here (its first
 //     step adds to 0), bit 26 the finished chain before it is
 //     stored at bits 13-24 (a byte offset into the wave's frame records: FrameRec::lm of its frame
 //     and band); without bit 26 the store goes to the lane's scratch word.
-//   ctl[(ngroups * chain_k(N) + stream) * 64 + lane]: the store of the stream's last chain (bit 26, bits 13-24).
+//   ctl[ngroups * 64 + lane]: the store of the lane's last chain (bit 26 and bits 13-24 only).
 //   w[track * ngroups * 8 + s]: the weight of the track's step s (0 past its last chain).
 struct ChainSched {
   int ngroups = 0;
@@ -357,9 +356,7 @@ struct ChainSched {
 static_assert(8 * (mgx::kChainMaxN / 2) - 1 <= 0x1FFF, "row offsets fit bits 0-12");
 static_assert(3 * mgx::kRecBytes + mgx::kRecLmOff + 4 * (mgx::kMaxMel - 1) <= 0xFFF, "record offsets fit bits 13-24");
 void chain_schedule(const int32_t* b, int nf, int L, int F, ChainSched& cs) {
-  // lane group t (lanes t F .. t F + F - 1) runs tracks t, t + nl, ..., one per stream, side by side
-  const int K = mgx::chain_k(2 * L);
-  const int nl = 64 / F, ntr = nl * K;
+  const int ntr = 64 / F;
   std::vector<int> lo(nf), len(nf), order;
   for (int j = 0; j < nf; ++j) {
     const int first = std::min<int>(b[j], L), end = std::min<int>(b[j + 2], L);
@@ -380,7 +377,7 @@ void chain_schedule(const int32_t* b, int nf, int L, int F, ChainSched& cs) {
   }
   const int ng = *std::max_element(load.begin(), load.end()) / 8;
   cs.ngroups = ng;
-  cs.ctl.assign((size_t)(ng + 1) * K * 64, 0u);
+  cs.ctl.assign((size_t)(ng + 1) * 64, 0u);
   cs.w.assign((size_t)ntr * ng * 8, 0.0);
   auto target = [&](int j, int f) {  // byte offset of FrameRec::lm[band (+32: a pair's first batch)]
     const int lmo = (F == 8 && f < 4) ? 32 : 0;
@@ -399,20 +396,20 @@ void chain_schedule(const int32_t* b, int nf, int L, int F, ChainSched& cs) {
         w[g0 * 8 + s] = v;
       }
       for (int f = 0; f < F; ++f) {
-        const int lane = (t % nl) * F + f, st = t / nl;
+        const int lane = t * F + f;
         for (int g = g0; g < g0 + len[j] / 8; ++g) {
           uint32_t c32 = (uint32_t)(f * L + lo[j] + 8 * (g - g0));
           if (g == g0) c32 |= 1u << 25 | (c > 0 ? target(track[t][c - 1], f) : 0u);
-          cs.ctl[((size_t)g * K + st) * 64 + lane] = c32;
+          cs.ctl[(size_t)g * 64 + lane] = c32;
         }
       }
       g0 += len[j] / 8;
     }
     for (int f = 0; f < F; ++f) {
-      const int lane = (t % nl) * F + f, st = t / nl;
+      const int lane = t * F + f;
       // past the track's last chain: bin 0 of the frame with zero weights (adds +0); no reset
-      for (int g = g0; g < ng; ++g) cs.ctl[((size_t)g * K + st) * 64 + lane] = (uint32_t)(f * L);
-      cs.ctl[((size_t)ng * K + st) * 64 + lane] = track[t].empty() ? 0u : target(track[t].back(), f);
+      for (int g = g0; g < ng; ++g) cs.ctl[(size_t)g * 64 + lane] = (uint32_t)(f * L);
+      cs.ctl[(size_t)ng * 64 + lane] = track[t].empty() ? 0u : target(track[t].back(), f);
     }
   }
 }
