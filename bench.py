@@ -149,6 +149,21 @@ def node_cpu(n, seconds, threads, fset="all", timeout_extra=120):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
+def cpu_quota():
+    """CPUs this process's cgroup may use (cpu.max / cfs quota), or None without a quota."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(n, seconds):
     """The reference's Node/jsfft CPU path as the build's JavaScript restatement
     (oracle/js/meyda_cpu.js, bit-exact to the reference's golden outputs), in the
@@ -172,13 +187,16 @@ def cpu_baseline(n, seconds):
             aff = len(os.sched_getaffinity(0))
         except (AttributeError, OSError):
             aff = allc
+        quota = cpu_quota()
         try:
             a = node_cpu(n, seconds, allc, timeout_extra=300)
             out["all_cores"] = {"value": a["value"], "unit": "frames/s", "cores": allc, "schedulable_cpus": aff,
-                                "kind": "js-restatement",
+                                "cgroup_cpu_quota": quota, "kind": "js-restatement",
                                 "sample": "%d frames (N=%d, all features) over %.1f s on %d worker_threads "
-                                          "(os.cpus().length; %d CPUs in this process's affinity mask)"
-                                          % (a["frames"], n, a["seconds"], allc, aff)}
+                                          "(os.cpus().length; %d CPUs in this process's affinity mask, cgroup CPU quota %s: "
+                                          "threads beyond the quota time-share it, each paying its own JIT warm-up)"
+                                          % (a["frames"], n, a["seconds"], allc, aff,
+                                             "%.1f CPUs" % quota if quota else "none")}
         except Exception as e:  # a report, never the measurement itself
             out["all_cores"] = {"value": None, "cores": allc, "note": "failed: %r" % (e,)}
         cfgs = {}

@@ -67,6 +67,7 @@ class Meyda {
       batchFrames: 1,
     }, options || {});
     this._ring = null;        // queued buffers (batchFrames > 1)
+    this._flushing = null;    // the ring whose frames a flush is delivering
     this._ringCount = 0;
     this.featureExtractors = {}; // user plugins: fn(bufferSize, m) or {process(signal)}
     this.EXTRACTION_STARTED = false;
@@ -93,6 +94,22 @@ class Meyda {
       }
       if (src && typeof src.connect === 'function') src.connect(this.spn, 0, 0);
     }
+  }
+
+  // `signal`: the current buffer (src/meyda.js:70). In a batched callback it is a view of the queued
+  // frames, made on first read.
+  get signal() {
+    if (this._sigBatch) {
+      const i = this._sigIndex, N = this.bufferSize;
+      this._sig = this._sigBatch.subarray(i * N, i * N + N);
+      this._sigBatch = null;
+    }
+    return this._sig;
+  }
+
+  set signal(v) {
+    this._sig = v;
+    this._sigBatch = null;
   }
 
   _window() {
@@ -163,7 +180,9 @@ class Meyda {
       this._callback(this.get(this._featuresToExtract));
       return;
     }
-    if (!this._ring) this._ring = new Float32Array(K * this.bufferSize);
+    if (!this._ring || this._ring === this._flushing || this._ring.length !== K * this.bufferSize) {
+      this._ring = new Float32Array(K * this.bufferSize);
+    }
     this._ring.set(signal, this._ringCount * this.bufferSize);
     if (++this._ringCount === K) this.flush();
   }
@@ -199,53 +218,27 @@ class Meyda {
   }
 
   // flush() for built-in features only: one launch, then each callback gets its frame's values as
-  // views into the batch's result arrays (numbers, and subarrays where get() returns arrays) instead
-  // of per-frame copies and a get() dispatch per buffer. The batch's arrays are fresh per launch, so
-  // a view stays valid after its callback. The queued frames move to the batch (the next process()
-  // starts a new ring), so `signal` -- and 'buffer' -- are views of them, as the buffer each callback
-  // describes. get() inside a callback recomputes that buffer's features.
+  // views into the batch's result arrays (numbers, and subarrays where get() returns arrays), built by
+  // one compiled object literal per feature list (frameBuilder) instead of per-frame copies and a get()
+  // dispatch per buffer. The batch's result arrays are fresh per launch, so a view stays valid after its
+  // callback. `signal` is a view of the queued frames, made only if read (the ring is reused by the
+  // next batch); 'buffer' is a copy of the frame.
   _flushViews(count, list, names) {
-    const N = this.bufferSize, L = N >> 1, nc = this.options.numMfccCoeffs || 13;
+    const N = this.bufferSize, nc = this.options.numMfccCoeffs || 13;
     const frames = this._ring.subarray(0, count * N);
-    this._ring = null;
+    this._flushing = this._ring;  // (a process() from a callback starts a new ring: these frames stay put)
     const gpu = Array.from(new Set(names.filter((n) => n !== 'buffer')));
     const r = gpu.length ? addon.extract(this._plan(), frames, gpu) : {};
-    const take = (name) => {
-      switch (name) {
-        case 'buffer': return (i) => frames.subarray(i * N, i * N + N);
-        case 'loudness': {
-          const sp = r['loudness.specific'], tot = r['loudness.total'];
-          return (i) => ({ specific: sp.subarray(i * 24, i * 24 + 24), total: tot[i] });
-        }
-        case 'mfcc': { const a = r.mfcc; return (i) => a.subarray(i * nc, i * nc + nc); }
-        case 'amplitudeSpectrum': { const a = r.amplitudeSpectrum; return (i) => a.subarray(i * L, i * L + L); }
-        case 'powerSpectrum': { const a = r.powerSpectrum; return (i) => a.subarray(i * L, i * L + L); }
-        case 'complexSpectrum': {
-          const re = r['complexSpectrum.real'], im = r['complexSpectrum.imag'];
-          return (i) => ({ real: re.subarray(i * N, i * N + N), imag: im.subarray(i * N, i * N + N), length: N });
-        }
-        default: { const a = r[name]; return (i) => a[i]; }
-      }
-    };
     const keep = this.signal;
     const cb = this._callback;
-    if (typeof list === 'string') {
-      const t = take(list);
-      for (let i = 0; i < count; i++) {
-        this.signal = frames.subarray(i * N, i * N + N);
-        this._frame = null;
-        cb(t(i));
-      }
-    } else {
-      const k = names.length, ts = names.map(take);
-      for (let i = 0; i < count; i++) {
-        this.signal = frames.subarray(i * N, i * N + N);
-        this._frame = null;
-        const out = {};
-        for (let j = 0; j < k; j++) out[names[j]] = ts[j](i);
-        cb(out);
-      }
+    const build = frameBuilder(typeof list === 'string' ? null : names, typeof list === 'string' ? list : null);
+    for (let i = 0; i < count; i++) {
+      this._sigBatch = frames;
+      this._sigIndex = i;
+      this._frame = null;
+      cb(build(r, frames, i, N, nc));
     }
+    this._flushing = null;
     this.signal = keep;
     this._frame = null;
   }
@@ -367,6 +360,32 @@ class Meyda {
     this._plans = {};
     this._asyncPlans = {};
   }
+}
+
+// A batched callback's value for frame i, compiled once per feature list: an object literal (or, for a
+// single name, the bare value) whose entries read the batch's result arrays -- numbers, and subarray
+// views where get() returns arrays -- so a callback costs an allocation, not a dispatch per feature.
+const BUILDERS = new Map();
+function frameBuilder(names, single) {
+  const key = single !== null ? '=' + single : names.join('\u0000');
+  let f = BUILDERS.get(key);
+  if (f) return f;
+  const expr = (n) => {
+    switch (n) {
+      case 'buffer': return 'x.slice(i * N, i * N + N)';
+      case 'loudness': return "{ specific: r['loudness.specific'].subarray(i * 24, i * 24 + 24), total: r['loudness.total'][i] }";
+      case 'mfcc': return 'r.mfcc.subarray(i * nc, i * nc + nc)';
+      case 'amplitudeSpectrum': case 'powerSpectrum': return 'r.' + n + '.subarray(i * (N >> 1), i * (N >> 1) + (N >> 1))';
+      case 'complexSpectrum': return "{ real: r['complexSpectrum.real'].subarray(i * N, i * N + N), " +
+        "imag: r['complexSpectrum.imag'].subarray(i * N, i * N + N), length: N }";
+      default: return 'r[' + JSON.stringify(n) + '][i]';
+    }
+  };
+  const body = single !== null ? expr(single)
+    : '{ ' + names.map((n) => JSON.stringify(n) + ': ' + expr(n)).join(', ') + ' }';
+  f = new Function('r', 'x', 'i', 'N', 'nc', 'return (' + body + ');');  // eslint-disable-line no-new-func
+  BUILDERS.set(key, f);
+  return f;
 }
 
 function toF32(frames) {

@@ -25,6 +25,12 @@ def test_facade_host_side():
     assert "facade_cpu: 8 checks passed" in out
 
 
+def test_facade_batched_delivery_host_side():
+    """The batched callback path's JavaScript logic against a stand-in addon (no GPU)."""
+    out = run_node("facade_batch.js")
+    assert "facade_batch: 4 checks passed" in out
+
+
 @pytest.mark.gpu
 def test_facade_on_gpu():
     out = run_node("facade_gpu.js")
