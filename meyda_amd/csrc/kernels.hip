@@ -311,6 +311,18 @@ __device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))
 #define MGX_MARK(tag) ((void)0)
 #endif
 
+// Phase stamps of the diagnostic build (-DMGX_WAVE_TIMES=1 only; tools/small_stamps.py): the 100 MHz
+// real-time clock at MGX_STAMP(i), written by the first lane of the first workgroup.
+#if MGX_WAVE_TIMES
+__device__ unsigned long long g_stamps[16];
+#define MGX_STAMP(i)                                                                              \
+  do {                                                                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0) ((volatile unsigned long long*)g_stamps)[i] = wall_clock64(); \
+  } while (0)
+#else
+#define MGX_STAMP(i) ((void)0)
+#endif
+
 // Wave-level LDS ordering (no global-memory fence: in-flight prefetch loads stay in flight).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -1205,6 +1217,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
     prio_lo<16>();
     MGX_MARK(stage0_done);
+    MGX_STAMP(3);
     GTw tw = gbl(ap->t.tw);
     GTwf twf = gbl(ap->t.twf);
     GTw twm = gbl(ap->t.twm);
@@ -1224,6 +1237,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       run_passes<N, 0, FAITH, false, TWL>(v, lpf, buf, tw, twf, twm, twl);
     }
     MGX_MARK(fft_done);
+    MGX_STAMP(4);
     prio_hi<32>();
     const bool want_cplx = ap->out.complex_real != nullptr;
     // src/meyda.js:104-114: |X_k| for k < N/2, rounded to float32.
@@ -1258,6 +1272,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     }
     prio_lo<32>();
     MGX_MARK(amp_done);
+    MGX_STAMP(5);
     wave_sync();  // the last exchange's reads are done: the slot buffer is free
     if (want_cplx) {
       // natural-order half spectrum X[0..N/2] in the slot buffer
@@ -1454,6 +1469,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
   const int roll_m = (total > thr) ? cnt - 1 : L;
   MGX_MARK(prefix_done);
+  MGX_STAMP(6);
   // The lane's mel records, then (G::PF == 2) the next frame: issued after the last table
   // load this frame waits on before them, so no wait of this frame is held up by the
   // prefetch; the band and mel sums, the moment finish and phase 2 run while it is in
@@ -1501,6 +1517,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // same path (a total of 2^64 or more is the cheap, conservative test: the path is the
   // reference's own summation, right for any frame).
   MGX_MARK(bands_done);
+  MGX_STAMP(7);
   const bool nonfinite = light ? light_nonfinite : !(total < 0x1p64);
   if (nonfinite) {
     // (CHAIN with paired batches: the pair's first batch keeps its mel sums in the upper half of lm)
@@ -1539,6 +1556,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   }
   prio_lo<8>();
   MGX_MARK(frame_end);
+  MGX_STAMP(8);
   wave_sync();  // pbuf reads done before the next frame's exchanges reuse the buffer
 }
 
@@ -1809,7 +1827,8 @@ __device__ __forceinline__ void done_signal(KArgs* q, int lane) {
 
 #if MGX_WAVE_TIMES
 // (diagnostic build only, tools/wave_times.py) per wave: start, after the prologue, end (the
-// 100 MHz real-time clock) and the CU id / workgroup
+// 100 MHz real-time clock) and the CU id / workgroup; and the first wave's phase stamps of its first
+// frame (g_stamps[i] at MGX_STAMP(i), tools/small_stamps.py: where a one-frame launch's time goes)
 __device__ unsigned long long g_wave_times[65536 * 4];
 #endif
 
@@ -1834,6 +1853,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   KArgs* ap = args_ptr();
 #if MGX_WAVE_TIMES
   const unsigned long long wt0 = wall_clock64();
+  MGX_STAMP(0);
 #endif
 
   // Kernel constants and the DCT table, once per workgroup (the only workgroup barrier).
@@ -1859,6 +1879,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   lds_barrier();
 #if MGX_WAVE_TIMES
   const unsigned long long wt1 = wall_clock64();
+  MGX_STAMP(1);
 #endif
 
   int lp[G::NPASS];
@@ -1967,6 +1988,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   float xn[G::PREFETCH ? CH : 1];
   if constexpr (G::PREFETCH) load(xn, b0, 0);
 
+  MGX_STAMP(2);
   int it = 0;  // the wave's batch count (CHAIN with paired batches: the pair's second when odd)
   for (uint64_t b = b0; b < bend; b += wstride, ++it) {
     const uint64_t f0 = b * FPW;
@@ -2001,6 +2023,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     // Lane ids and the argument pointer are re-derived so that nothing phase 2 needs is
     // hoisted out of the batch loop (it would stay live across the FFT).
     MGX_MARK(phase2_start);
+    MGX_STAMP(9);
     prio_hi<4>();
     // CHAIN: the mel chains, then the log and the DCT, every batch -- or with paired batches
     // (chain_pair) every second batch of the wave, for the pair (its first batch's energies in the
@@ -2105,6 +2128,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     }
     prio_lo<4>();
     MGX_MARK(phase2_end);
+    MGX_STAMP(10);
     wave_sync();  // records and slot buffer are reused by the next batch
     // The workgroup's four waves meet after every second group of 16 frames (G::GROUP_SYNC).
     // Left alone they drift apart by more than the L2's turnover time, so each wave's 16-byte piece
@@ -2156,7 +2180,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       prio_lo<4>();
     }
   }
+  MGX_STAMP(11);
   if (args_ptr()->done_flag) done_signal(args_ptr(), opaque(lane));
+  MGX_STAMP(12);
 #if MGX_WAVE_TIMES
   if (lane == 0 && blockIdx.x < 16384) {
     auto g = (__attribute__((address_space(1))) unsigned long long*)g_wave_times + ((uint64_t)blockIdx.x * 4 + wave) * 4;
@@ -2368,6 +2394,9 @@ hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t firs
 }  // namespace mgx
 
 #if MGX_WAVE_TIMES
+extern "C" int mgx_debug_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mgx::g_stamps), 16 * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 extern "C" int mgx_debug_wave_times(unsigned long long* host, int count) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(mgx::g_wave_times), (size_t)count * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
