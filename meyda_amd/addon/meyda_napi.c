@@ -506,6 +506,94 @@ static napi_value extract_common(napi_env env, napi_callback_info info, int wav)
   return r;
 }
 
+/* extractInto(plan, frames, offsets, out): the same synchronous extraction into ONE caller-provided
+ * ArrayBuffer. offsets: a Float64Array of the 19 output fields' byte offsets in `out` (mgx_outputs
+ * order: the 13 scalars, loudness_specific, mfcc, amplitude, power, complex real, complex imag; a
+ * negative entry = not requested). The facade's real-time paths (get(), batched streaming) lay the
+ * outputs of a feature list out once and call this per buffer or batch: one allocation and a handful of
+ * N-API calls instead of an ArrayBuffer, a reference and a typed array per output. */
+static napi_value extract_into(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 4) {
+    napi_throw_type_error(env, NULL, "extractInto(plan, frames, offsets, out)");
+    return NULL;
+  }
+  plan_box* box = get_plan(env, argv[0]);
+  if (!box) return NULL;
+  if (box->busy) {
+    napi_throw_error(env, NULL, "plan is busy with an async extraction");
+    return NULL;
+  }
+  napi_typedarray_type tt;
+  size_t len = 0, off = 0, olen = 0;
+  void* data = NULL;
+  void* offs = NULL;
+  napi_value ab;
+  bool is = false;
+  napi_is_typedarray(env, argv[1], &is);
+  if (is) napi_get_typedarray_info(env, argv[1], &tt, &len, &data, &ab, &off);
+  if (!is || tt != napi_float32_array) {
+    napi_throw_type_error(env, NULL, "frames must be a Float32Array");
+    return NULL;
+  }
+  napi_is_typedarray(env, argv[2], &is);
+  if (is) napi_get_typedarray_info(env, argv[2], &tt, &olen, &offs, &ab, &off);
+  if (!is || tt != napi_float64_array || olen != 19) {
+    napi_throw_type_error(env, NULL, "offsets must be a Float64Array of 19 byte offsets");
+    return NULL;
+  }
+  void* out = NULL;
+  size_t out_bytes = 0;
+  napi_is_arraybuffer(env, argv[3], &is);
+  if (is) napi_get_arraybuffer_info(env, argv[3], &out, &out_bytes);
+  if (!is) {
+    napi_throw_type_error(env, NULL, "out must be an ArrayBuffer");
+    return NULL;
+  }
+  const uint32_t n = box->desc.buffer_size;
+  if (len % n) {
+    napi_throw_range_error(env, NULL, "frames.length must be a multiple of bufferSize");
+    return NULL;
+  }
+  const uint64_t F = len / n;
+  const size_t ss = box->desc.scalar_f64 ? 8 : 4;
+  size_t per[19];
+  for (int i = 0; i < 19; ++i)
+    per[i] = i < MGX_NUM_SCALARS ? ss : i == 13 ? 24 * 4 : i == 14 ? (size_t)box->desc.num_mfcc_coeffs * 4
+           : i < 17 ? (size_t)(n / 2) * 4 : (size_t)n * 4;
+  void* ptr[19];
+  const double* o = (const double*)offs;
+  for (int i = 0; i < 19; ++i) {
+    ptr[i] = NULL;
+    if (!(o[i] >= 0)) continue;
+    const double end = o[i] + (double)(per[i] * F);
+    if (o[i] != (double)(uint64_t)o[i] || end > (double)out_bytes || ((uint64_t)o[i] % (i < MGX_NUM_SCALARS ? ss : 4))) {
+      napi_throw_range_error(env, NULL, "an output's offset is misaligned or runs past the end of out");
+      return NULL;
+    }
+    ptr[i] = (unsigned char*)out + (uint64_t)o[i];
+  }
+  if ((ptr[17] == NULL) != (ptr[18] == NULL)) {
+    napi_throw_range_error(env, NULL, "complex real and imag go together");
+    return NULL;
+  }
+  mgx_outputs mo;
+  memset(&mo, 0, sizeof mo);
+  for (int i = 0; i < MGX_NUM_SCALARS; ++i) mo.scalars[i] = ptr[i];
+  mo.loudness_specific = (float*)ptr[13];
+  mo.mfcc = (float*)ptr[14];
+  mo.amplitude_spectrum = (float*)ptr[15];
+  mo.power_spectrum = (float*)ptr[16];
+  mo.complex_real = (float*)ptr[17];
+  mo.complex_imag = (float*)ptr[18];
+  const int rc = box->group ? mgx_group_extract_host(box->group, (const float*)data, F, &mo)
+                            : mgx_extract_host(box->plan, (const float*)data, F, &mo);
+  if (rc) return throw_mgx(env, rc);
+  return argv[3];
+}
+
 static napi_value extract_sync(napi_env env, napi_callback_info info) { return extract_common(env, info, 0); }
 static napi_value extract_wav_sync(napi_env env, napi_callback_info info) { return extract_common(env, info, 1); }
 
@@ -689,6 +777,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"destroyPlan", NULL, destroy_plan, NULL, NULL, NULL, napi_enumerable, NULL},
       {"planBusy", NULL, plan_busy, NULL, NULL, NULL, napi_enumerable, NULL},
       {"extract", NULL, extract_sync, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"extractInto", NULL, extract_into, NULL, NULL, NULL, napi_enumerable, NULL},
       {"extractAsync", NULL, extract_async, NULL, NULL, NULL, napi_enumerable, NULL},
       {"extractWav", NULL, extract_wav_sync, NULL, NULL, NULL, napi_enumerable, NULL},
       {"extractWavAsync", NULL, extract_wav_async, NULL, NULL, NULL, napi_enumerable, NULL},

@@ -228,7 +228,7 @@ class Meyda {
     const frames = this._ring.subarray(0, count * N);
     this._flushing = this._ring;  // (a process() from a callback starts a new ring: these frames stay put)
     const gpu = Array.from(new Set(names.filter((n) => n !== 'buffer')));
-    const r = gpu.length ? addon.extract(this._plan(), frames, gpu) : {};
+    const r = gpu.length ? extractViews(this._plan(), frames, gpu, N, nc) : {};
     const keep = this.signal;
     const cb = this._callback;
     const build = frameBuilder(typeof list === 'string' ? null : names, typeof list === 'string' ? list : null);
@@ -289,7 +289,7 @@ class Meyda {
     if (!this._frame) this._frame = {};
     const need = names.filter((n) => !(n in this._frame));
     if (!need.length) return;
-    const r = addon.extract(this._plan(), this._signal(), need);
+    const r = extractViews(this._plan(), this._signal(), need, this.bufferSize, this.options.numMfccCoeffs);
     for (const n of need) this._frame[n] = frameValue(n, r, 0, this.bufferSize, this.options.numMfccCoeffs);
   }
 
@@ -360,6 +360,48 @@ class Meyda {
     this._plans = {};
     this._asyncPlans = {};
   }
+}
+
+// The output fields of the C ABI in mgx_outputs order (the addon's extractInto offsets) and the result
+// keys each requested feature fills.
+const FIELDS = ['rms', 'energy', 'zcr', 'spectralCentroid', 'spectralFlatness', 'spectralSlope', 'spectralRolloff',
+  'spectralSpread', 'spectralSkewness', 'spectralKurtosis', 'loudness.total', 'perceptualSpread', 'perceptualSharpness',
+  'loudness.specific', 'mfcc', 'amplitudeSpectrum', 'powerSpectrum', 'complexSpectrum.real', 'complexSpectrum.imag'];
+const KEYS_OF = { loudness: ['loudness.specific', 'loudness.total'],
+  complexSpectrum: ['complexSpectrum.real', 'complexSpectrum.imag'] };
+
+// Extraction of F frames into one fresh ArrayBuffer (addon.extractInto), its layout worked out once per
+// (feature list, F): a result object of typed-array views with extract()'s keys and shapes (scalars as
+// Float64Array: the facade's plans use scalarF64). One allocation and a few N-API calls per launch
+// instead of an ArrayBuffer, a reference and a typed array per output (the real-time paths).
+const LAYOUTS = new Map();
+function extractViews(plan, frames, names, N, nc) {
+  const F = frames.length / N;
+  const key = F + '|' + N + '|' + nc + '|' + names.join('\u0000');
+  let lay = LAYOUTS.get(key);
+  if (!lay) {
+    const want = new Set();
+    for (const n of names) for (const k of KEYS_OF[n] || [n]) want.add(k);
+    const per = (i) => (i < 13 ? 1 : i === 13 ? 24 : i === 14 ? nc : i < 17 ? N / 2 : N);
+    const offsets = new Float64Array(19).fill(-1);
+    const views = [];
+    let at = 0;
+    FIELDS.forEach((k, i) => {
+      if (!want.has(k)) return;
+      const len = F * per(i), bytes = len * (i < 13 ? 8 : 4);
+      offsets[i] = at;
+      views.push([k, i < 13 ? Float64Array : Float32Array, at, len]);
+      at += Math.ceil(bytes / 8) * 8;
+    });
+    lay = { offsets, views, bytes: Math.max(at, 8) };
+    if (LAYOUTS.size > 256) LAYOUTS.clear();
+    LAYOUTS.set(key, lay);
+  }
+  const ab = new ArrayBuffer(lay.bytes);
+  addon.extractInto(plan, frames, lay.offsets, ab);
+  const r = {};
+  for (const [k, T, off, len] of lay.views) r[k] = new T(ab, off, len);
+  return r;
 }
 
 // A batched callback's value for frame i, compiled once per feature list: an object literal (or, for a

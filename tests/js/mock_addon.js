@@ -13,6 +13,20 @@ module.exports = {
   destroyPlan: () => {},
   planBusy: () => false,
   isPowerOfTwo: (v) => v > 0 && (v & (v - 1)) === 0,
+  // extractInto(plan, frames, offsets, out): the same values at the facade's byte offsets (mgx_outputs
+  // field order; scalars float64, as the facade's plans ask)
+  extractInto: (plan, frames, offsets, out) => {
+    const N = plan.o.bufferSize, F = frames.length / N;
+    calls.push({ F, into: true, fields: Array.from(offsets).map((o, i) => (o >= 0 ? i : -1)).filter((i) => i >= 0) });
+    const base = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 99, 10, 11, 100, 200, 300, 300, 400, 500];
+    for (let i = 0; i < 19; i++) {
+      if (!(offsets[i] >= 0)) continue;
+      const per = i < 13 ? 1 : i === 13 ? 24 : i === 14 ? 13 : i < 17 ? N / 2 : N;
+      const a = i < 13 ? new Float64Array(out, offsets[i], F) : new Float32Array(out, offsets[i], F * per);
+      for (let f = 0; f < F; f++) for (let k = 0; k < per; k++) a[f * per + k] = frames[f * N] + base[i] + k;
+    }
+    return out;
+  },
   extract: (plan, frames, names) => {
     const N = plan.o.bufferSize, F = frames.length / N, r = {};
     calls.push({ F, names: names.slice() });
