@@ -2022,8 +2022,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     // ------------------------------------------------------------- phase 2
     // Lane ids and the argument pointer are re-derived so that nothing phase 2 needs is
     // hoisted out of the batch loop (it would stay live across the FFT).
-    MGX_MARK(phase2_start);
     MGX_STAMP(9);
+    MGX_MARK(phase2_start);
     prio_hi<4>();
     // CHAIN: the mel chains, then the log and the DCT, every batch -- or with paired batches
     // (chain_pair) every second batch of the wave, for the pair (its first batch's energies in the
