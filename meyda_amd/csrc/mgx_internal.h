@@ -12,10 +12,8 @@ constexpr int kMaxMel = 64;
 // scalar_pass), one lane per frame: the window's per-frame inputs (10 8-byte words each, the
 // record's S[0..4], ln2sum, energy, loudness total, zcr | roll_m, loud_max | sharp_sum) wait in
 // device memory, kScalWords words per wave.
-#ifndef MGX_SCAL_BATCHES
-#define MGX_SCAL_BATCHES 16
-#endif
-constexpr int kScalBatches = MGX_SCAL_BATCHES;
+// (a constant: the round-4 override macro built window lengths that no test covered)
+constexpr int kScalBatches = 16;
 // word c of the window's frame l (l = 4 batch + frame, < 4 kScalBatches) at c * 64 + l
 static_assert(4 * kScalBatches <= 64, "a window's frames are lanes of one wave");
 constexpr int kScalWords = 10 * 64;
