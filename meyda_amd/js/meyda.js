@@ -68,6 +68,7 @@ class Meyda {
     }, options || {});
     this._ring = null;        // queued buffers (batchFrames > 1)
     this._flushing = null;    // the ring whose frames a flush is delivering
+    this._layouts = new Map(); // extractViews' output layouts, per (fields, frames)
     this._ringCount = 0;
     this.featureExtractors = {}; // user plugins: fn(bufferSize, m) or {process(signal)}
     this.EXTRACTION_STARTED = false;
@@ -228,7 +229,7 @@ class Meyda {
     const frames = this._ring.subarray(0, count * N);
     this._flushing = this._ring;  // (a process() from a callback starts a new ring: these frames stay put)
     const gpu = Array.from(new Set(names.filter((n) => n !== 'buffer')));
-    const r = gpu.length ? extractViews(this._plan(), frames, gpu, N, nc) : {};
+    const r = gpu.length ? extractViews(this._layouts, this._plan(), frames, gpu, N, nc) : {};
     const keep = this.signal;
     const cb = this._callback;
     const build = frameBuilder(typeof list === 'string' ? null : names, typeof list === 'string' ? list : null);
@@ -289,7 +290,7 @@ class Meyda {
     if (!this._frame) this._frame = {};
     const need = names.filter((n) => !(n in this._frame));
     if (!need.length) return;
-    const r = extractViews(this._plan(), this._signal(), need, this.bufferSize, this.options.numMfccCoeffs);
+    const r = extractViews(this._layouts, this._plan(), this._signal(), need, this.bufferSize, this.options.numMfccCoeffs);
     for (const n of need) this._frame[n] = frameValue(n, r, 0, this.bufferSize, this.options.numMfccCoeffs);
   }
 
@@ -370,37 +371,44 @@ const FIELDS = ['rms', 'energy', 'zcr', 'spectralCentroid', 'spectralFlatness', 
 const KEYS_OF = { loudness: ['loudness.specific', 'loudness.total'],
   complexSpectrum: ['complexSpectrum.real', 'complexSpectrum.imag'] };
 
+// Output-field bits of each feature name (its FIELDS entries).
+const FIELD_BITS = {};
+FIELDS.forEach((k, i) => { FIELD_BITS[k] = 2 ** i; });
+FIELD_BITS.loudness = FIELD_BITS['loudness.specific'] + FIELD_BITS['loudness.total'];
+FIELD_BITS.complexSpectrum = FIELD_BITS['complexSpectrum.real'] + FIELD_BITS['complexSpectrum.imag'];
+
 // Extraction of F frames into one fresh ArrayBuffer (addon.extractInto), its layout worked out once per
-// (feature list, F): a result object of typed-array views with extract()'s keys and shapes (scalars as
-// Float64Array: the facade's plans use scalarF64). One allocation and a few N-API calls per launch
-// instead of an ArrayBuffer, a reference and a typed array per output (the real-time paths).
-const LAYOUTS = new Map();
-function extractViews(plan, frames, names, N, nc) {
+// (output fields, F) and kept in the instance's `cache`: a result object of typed-array views with
+// extract()'s keys and shapes (scalars as Float64Array: the facade's plans use scalarF64). One
+// allocation and a few N-API calls per launch instead of an ArrayBuffer, a reference and a typed array
+// per output (the real-time paths).
+function extractViews(cache, plan, frames, names, N, nc) {
   const F = frames.length / N;
-  const key = F + '|' + N + '|' + nc + '|' + names.join('\u0000');
-  let lay = LAYOUTS.get(key);
+  let bits = 0;
+  for (let j = 0; j < names.length; j++) bits += FIELD_BITS[names[j]] || 0;  // (names are distinct)
+  const key = F < 4194304 ? bits * 4194304 + F : bits + ':' + F;
+  let lay = cache.get(key);
   if (!lay) {
-    const want = new Set();
-    for (const n of names) for (const k of KEYS_OF[n] || [n]) want.add(k);
     const per = (i) => (i < 13 ? 1 : i === 13 ? 24 : i === 14 ? nc : i < 17 ? N / 2 : N);
     const offsets = new Float64Array(19).fill(-1);
     const views = [];
     let at = 0;
     FIELDS.forEach((k, i) => {
-      if (!want.has(k)) return;
+      if (!(Math.floor(bits / 2 ** i) % 2)) return;
       const len = F * per(i), bytes = len * (i < 13 ? 8 : 4);
       offsets[i] = at;
       views.push([k, i < 13 ? Float64Array : Float32Array, at, len]);
       at += Math.ceil(bytes / 8) * 8;
     });
     lay = { offsets, views, bytes: Math.max(at, 8) };
-    if (LAYOUTS.size > 256) LAYOUTS.clear();
-    LAYOUTS.set(key, lay);
+    if (cache.size > 256) cache.clear();
+    cache.set(key, lay);
   }
   const ab = new ArrayBuffer(lay.bytes);
   addon.extractInto(plan, frames, lay.offsets, ab);
   const r = {};
-  for (const [k, T, off, len] of lay.views) r[k] = new T(ab, off, len);
+  const v = lay.views;
+  for (let j = 0; j < v.length; j++) r[v[j][0]] = new v[j][1](ab, v[j][2], v[j][3]);
   return r;
 }
 
