@@ -291,6 +291,34 @@ check('options.devices: batches through a device group equal the single-device p
   });
 });
 
+check('addon extractInto: one buffer, caller offsets, equal to extract(); bad offsets rejected', () => {
+  const addon = Meyda.addon;
+  const plan = addon.createPlan({ bufferSize: 512, sampleRate: 44100, scalarF64: 1 });
+  const F = 9;
+  const x = g.input.subarray(0, F * 512);
+  const want = addon.extract(plan, x, ['rms', 'zcr', 'loudness', 'mfcc', 'amplitudeSpectrum']);
+  const off = new Float64Array(19).fill(-1);
+  // rms, zcr, loudness.total (f64) then loudness.specific, mfcc, amplitude (f32), packed back to back
+  off[0] = 0; off[2] = 8 * F; off[10] = 16 * F; off[13] = 24 * F; off[14] = off[13] + 96 * F; off[15] = off[14] + 52 * F;
+  const ab = new ArrayBuffer(off[15] + 4 * 256 * F);
+  assert.strictEqual(addon.extractInto(plan, x, off, ab), ab);
+  const same = (a, b, k) => assert.deepStrictEqual(Array.from(a), Array.from(b), k);
+  same(new Float64Array(ab, off[0], F), want.rms, 'rms');
+  same(new Float64Array(ab, off[2], F), want.zcr, 'zcr');
+  same(new Float64Array(ab, off[10], F), want['loudness.total'], 'loudness.total');
+  same(new Float32Array(ab, off[13], 24 * F), want['loudness.specific'], 'loudness.specific');
+  same(new Float32Array(ab, off[14], 13 * F), want.mfcc, 'mfcc');
+  same(new Float32Array(ab, off[15], 256 * F), want.amplitudeSpectrum, 'amplitude');
+  const bad1 = Float64Array.from(off); bad1[0] = 4;   // an f64 output at a 4-byte offset
+  assert.throws(() => addon.extractInto(plan, x, bad1, ab), /misaligned|past the end/);
+  const bad2 = Float64Array.from(off); bad2[15] = ab.byteLength - 16;  // runs past the end
+  assert.throws(() => addon.extractInto(plan, x, bad2, ab), /past the end/);
+  const bad3 = Float64Array.from(off); bad3[17] = 0;  // complex real without imag
+  assert.throws(() => addon.extractInto(plan, x, bad3, ab), /go together|past the end/);
+  assert.throws(() => addon.extractInto(plan, x, new Float64Array(18), ab), /19 byte offsets/);
+  addon.destroyPlan(plan);
+});
+
 (async () => {
   for (const [name, fn] of checks) {
     await fn();
