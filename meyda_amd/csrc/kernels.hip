@@ -322,6 +322,15 @@ __device__ unsigned long long g_stamps[16];
 #else
 #define MGX_STAMP(i) ((void)0)
 #endif
+// (and the shader clock beside it, g_stamps[i] = clock64(): the core clock the one-frame launch ran at)
+#if MGX_WAVE_TIMES
+#define MGX_CLOCK_STAMP(i)                                                                        \
+  do {                                                                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0) ((volatile unsigned long long*)g_stamps)[i] = clock64(); \
+  } while (0)
+#else
+#define MGX_CLOCK_STAMP(i) ((void)0)
+#endif
 
 // Wave-level LDS ordering (no global-memory fence: in-flight prefetch loads stay in flight).
 __device__ __forceinline__ void wave_sync() {
@@ -1854,6 +1863,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
 #if MGX_WAVE_TIMES
   const unsigned long long wt0 = wall_clock64();
   MGX_STAMP(0);
+  MGX_CLOCK_STAMP(13);
 #endif
 
   // Kernel constants and the DCT table, once per workgroup (the only workgroup barrier).
@@ -2183,6 +2193,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   MGX_STAMP(11);
   if (args_ptr()->done_flag) done_signal(args_ptr(), opaque(lane));
   MGX_STAMP(12);
+  MGX_CLOCK_STAMP(14);
 #if MGX_WAVE_TIMES
   if (lane == 0 && blockIdx.x < 16384) {
     auto g = (__attribute__((address_space(1))) unsigned long long*)g_wave_times + ((uint64_t)blockIdx.x * 4 + wave) * 4;

@@ -4,7 +4,7 @@ library (tools/variant.sh wt -DMGX_WAVE_TIMES=1 -> ab/lib_wt.so) stamps the 100 
 at the phases of the first wave's frame (kernels.hip MGX_STAMP); this runs mgx_extract_host on one
 frame many times (the small host path: pinned mapped memory, completion word) and prints, for the
 last calls, the median time from the kernel's first instruction to each stamp, and the call's own
-duration on the host. usage: small_stamps.py LIB [N features ...]"""
+duration on the host, and the shader clock the launch ran at (clock64 ticks over real time). usage: small_stamps.py LIB [N features ...]"""
 import ctypes
 import json
 import sys
@@ -36,7 +36,7 @@ def main():
         x = np.random.default_rng(1).uniform(-1, 1, (1, n)).astype(np.float32)
         shim = types.SimpleNamespace(n=n, scalar_dtype=np.float64, desc=d)
         out, o = capi.Plan._host_outputs(shim, 1, feats)
-        stamps, calls = [], []
+        stamps, calls, sclk = [], [], []
         buf = (ctypes.c_ulonglong * 16)()
         for k in range(3000):
             t0 = time.perf_counter()
@@ -46,9 +46,11 @@ def main():
                 assert L.mgx_debug_stamps(buf) == 0
                 s = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
                 stamps.append((s[:13] - s[0]) * 10e-3)  # 100 MHz ticks -> us
+                sclk.append((s[14] - s[13]) / max(1, s[12] - s[0]) * 100.0)  # shader clocks per us -> MHz
         st = np.median(np.array(stamps), axis=0)
         print(json.dumps({"n": n, "features": len(feats), "host_call_us": float(np.median(calls[1000:]) * 1e6),
-                          "kernel_us_by_stamp": {NAMES[i]: round(float(st[i]), 2) for i in range(13)}}))
+                          "kernel_us_by_stamp": {NAMES[i]: round(float(st[i]), 2) for i in range(13)},
+                          "shader_clock_mhz": round(float(np.median(sclk)), 1)}))
 
 
 if __name__ == "__main__":
