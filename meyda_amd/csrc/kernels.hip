@@ -38,6 +38,7 @@ typedef const __attribute__((address_space(1))) float2* GTwf;
 typedef const __attribute__((address_space(1))) double* GD;
 typedef const __attribute__((address_space(1))) float* GF;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr double kS = 0.7071067811865476;  // Math.SQRT1_2 (lib/jsfft/fft.js:10)
 constexpr float kSf = 0.70710677f;
@@ -297,6 +298,10 @@ __device__ __forceinline__ void st_out(P p, float v) {
   __builtin_nontemporal_store(v, p);
 }
 
+// (A/B: -DMGX_NT_FRAMES=1 loads every kernel's frames non-temporally, as the CHAIN kernel's)
+#ifndef MGX_NT_FRAMES
+#define MGX_NT_FRAMES 0
+#endif
 template <bool NT = false>
 __device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))) float* p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -1097,7 +1102,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   auto prefetch_next = [&]() {
     if constexpr (G::PF == 2) {
 #pragma unroll
-      for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN>(next + (c * 64 + (unsigned)lane));
+      for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN || MGX_NT_FRAMES>(next + (c * 64 + (unsigned)lane));
     }
   };
   // The window: held in registers for the launch at N = 1024 (Geo::WIN_REG); otherwise its
@@ -1818,6 +1823,34 @@ __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
   }
 }
 
+// The workgroup's LDS tables (Lds<N>: the bark limits' prefix-row offsets, the tame passes' twiddles,
+// the DCT table) written at `base` = the image of LDS byte Lds<N>::kc_off + 128: lds_image_kernel writes
+// them once per plan to device memory, and every launch's prologue copies that image into LDS.
+template <int N, bool FAITH, bool LITERAL>
+__device__ void stage_tables(KArgs* ap, unsigned char* base) {
+  using LY = Lds<N>;
+  constexpr size_t at = LY::kc_off + 128;
+  int* klim = reinterpret_cast<int*>(base);
+  // the bark limits as byte offsets of their entries in the padded prefix row (band sums)
+  if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = 8 * pd(gbl(ap->t.bblim)[threadIdx.x - 64]);
+  if constexpr (Geo<N>::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
+    stage_twiddles<N, 1, 0>(reinterpret_cast<double2*>(base + (LY::twl_off - at)), gbl(ap->t.tw), gbl(ap->t.twm));
+  } else if constexpr (Geo<N>::TW_LDS && !FAITH && !LITERAL) {  // the fast precision's (TwLdsF)
+    float2* d = reinterpret_cast<float2*>(base + (LY::twl_off - at));
+    const GTwf src = gbl(ap->t.twf);
+    for (int i = threadIdx.x; i < TwLdsF<N>::count; i += kThreads) d[i] = ld_twf(src, TwLdsF<N>::first + i);
+  }
+  const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
+  const auto dct = gbl(ap->t.dct);
+  float* dd = reinterpret_cast<float*>(base + (LY::dct_off - at));
+  for (int i = threadIdx.x; i < ntp; i += kThreads) dd[i] = i < nt ? dct[i] : 0.0f;
+}
+
+template <int N, bool FAITH, bool LITERAL>
+__global__ __launch_bounds__(kThreads) void lds_image_kernel(KernelArgs a, unsigned char* image) {
+  stage_tables<N, FAITH, LITERAL>(args_ptr(), image);
+}
+
 // The completion word of a small host batch (KernelArgs::done_flag): this wave's output stores
 // complete and visible to the host (a system-scope release), then one count per wave from lane 0
 // (a vector atomic); the wave that makes the count whole resets it for the next launch and
@@ -1825,6 +1858,14 @@ __device__ __forceinline__ void stage_twiddles(double2* twl, GTw tw, GTw twm) {
 // waiting for the kernel's completion to reach the runtime (profiles/r04_small_latency.txt).
 __device__ __forceinline__ void done_signal(KArgs* q, int lane) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (gridDim.x == 1) {
+    // one workgroup (a real-time launch of at most 16 frames): its four waves meet at a barrier instead of
+    // counting themselves in device memory, and the first releases the word (no atomic round trip)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (threadIdx.x == 0) __hip_atomic_store(q->done_flag, q->done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   if (lane == 0) {
     const uint32_t before = __hip_atomic_fetch_add(q->done_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
     if (before + 1 == q->done_waves) {
@@ -1865,47 +1906,31 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   MGX_STAMP(0);
   MGX_CLOCK_STAMP(13);
 #endif
-
-  // Kernel constants and the DCT table, once per workgroup (the only workgroup barrier).
-  {
-    void** kptr = reinterpret_cast<void**>(smem + LY::kc_off);
-    int* klim = reinterpret_cast<int*>(smem + LY::kc_off + 16 * 8);
-    if (threadIdx.x < MGX_NUM_SCALARS) kptr[threadIdx.x] = ap->out.scalars[threadIdx.x];
-    // the bark limits as byte offsets of their entries in the padded prefix row (band sums)
-    if (threadIdx.x >= 64 && threadIdx.x < 64 + kBark + 1) klim[threadIdx.x - 64] = 8 * pd(gbl(ap->t.bblim)[threadIdx.x - 64]);
-  }
-  if constexpr (Geo<N>::TW_LDS && FAITH && !LITERAL) {  // the tame passes' twiddles (TwLds)
-    stage_twiddles<N, 1, 0>(reinterpret_cast<double2*>(smem + LY::twl_off), gbl(ap->t.tw), gbl(ap->t.twm));
-  } else if constexpr (Geo<N>::TW_LDS && !FAITH && !LITERAL) {  // the fast precision's (TwLdsF)
-    float2* d = reinterpret_cast<float2*>(smem + LY::twl_off);
-    const GTwf src = gbl(ap->t.twf);
-    for (int i = threadIdx.x; i < TwLdsF<N>::count; i += kThreads) d[i] = ld_twf(src, TwLdsF<N>::first + i);
-  }
-  if (ap->need_spectrum && ap->need_mfcc) {
-    const int nt = ap->ncoef * ap->nfilt, ntp = ap->ncoef * ((ap->nfilt + 7) & ~7);
-    const auto dct = gbl(ap->t.dct);
-    for (int i = threadIdx.x; i < ntp; i += kThreads) dct_lds[i] = i < nt ? dct[i] : 0.0f;
-  }
-  lds_barrier();
-#if MGX_WAVE_TIMES
-  const unsigned long long wt1 = wall_clock64();
-  MGX_STAMP(1);
-#endif
+  // The kernel arguments the prologue reads, loaded in one burst and waited for together (the empty asm
+  // keeps their loads here, ahead of every branch): a one-frame launch (the real-time path) then pays one
+  // round trip to the kernarg segment before its table and frame loads issue, not one per dependent step.
+  const uint64_t nf = ap->num_frames;
+  const uint32_t nr32 = (uint32_t)ap->wg_ranks, nimg = ap->t.lds_image_chunks, grid = gridDim.x;
+  const void* const img_p = ap->t.lds_image;
+  const float* const frames_p = ap->frames;
+  const float* const win_p = ap->t.window;
+  const int* const klist_p = ap->t.klist;
+  asm volatile("" ::"s"(nf), "s"(nr32), "s"(nimg), "s"(grid), "s"(img_p), "s"(frames_p), "s"(win_p), "s"(klist_p));
 
   int lp[G::NPASS];
 #pragma unroll
   for (int p = 0; p < G::NPASS; ++p) lp[p] = PG::lanepart(p, lane);
-  KlTab<N> kl;  // spectrum bin held by each register after the last pass
+  // (the bin list's loads issued here, read after the table staging below)
+  int kraw[R];
   {
-    const auto klist = gbl(ap->t.klist);
+    const auto klist = gbl(klist_p);
 #pragma unroll
-    for (int r = 0; r < R; ++r) kl.set(r, pa(klist[lp[G::NPASS - 1] | PG::rpart(G::NPASS - 1, r)]));
+    for (int r = 0; r < R; ++r) kraw[r] = klist[lp[G::NPASS - 1] | PG::rpart(G::NPASS - 1, r)];
   }
   const bool dc_lane = lp[G::NPASS - 1] == 0;
 
   // Every wave works through its own batches of FPW consecutive frames: phase 1 per
   // frame, then phase 2 over the batch, with wave-level synchronisation only.
-  const uint64_t nf = ap->num_frames;
   const uint64_t nb = (nf + FPW - 1) / FPW;
   // Each workgroup owns one contiguous range of batches, its 4 waves interleaved
   // (wave w takes batches 4k + w), so the 16 frames the waves finish together are
@@ -1919,13 +1944,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // Rank r takes a share of its own instead (22 / 18 / 14 / 10 of 64 at N = 1024).
   const uint64_t ng = (nb + 3) / 4;
   uint64_t g0, g1;
-  const uint64_t nr = (uint64_t)ap->wg_ranks;
+  const uint64_t nr = (uint64_t)nr32;
   // (unequal shares need many groups per workgroup: with a few each, their rounding unbalances
   // more than the ranks' rates do -- C2's 65,536 frames at N = 512 lost 6 %; and N = 256 lost 4 %)
   // (12 groups per workgroup: at 8-11 the rank shares' pair rounding cost more than the ranks'
   // rates gain -- 196,608 frames at N = 512 -5.0 %, 131,072 at 1024 -1.9 % with equal pairs instead;
   // below 8 equal pairs won by 2-16 %, profiles/r04_tuning.txt)
-  const bool many = ng >= 12 * (uint64_t)gridDim.x;
+  const bool many = ng >= 12 * (uint64_t)grid;
   // Every boundary between two workgroups' ranges falls on an even group (32 frames): the
   // 4-byte scalar outputs of a workgroup then fill whole 128-byte lines (and the 52-byte MFCC
   // and 96-byte loudness records whole lines too), so no output line is written from two
@@ -1940,28 +1965,28 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     g0 = a < hi ? a : hi;
     g1 = b < hi ? b : hi;
   };
-  if (N >= 512 && N != 1024 && many && nr >= 2 && nr <= 8 && gridDim.x % nr == 0) {
+  if (N >= 512 && N != 1024 && many && nr >= 2 && nr <= 8 && grid % nr == 0) {
     // other N: rank r's weight 5 (R - 1) - 2 r, from 5:3 for the first rank to the last (round 4: 2:1
     // before; 5:3 measured -1.2 % at N = 2048 and -0.9..-1.7 % at 512, steeper and flatter ones slower)
-    const uint64_t q = gridDim.x / nr, r = blockIdx.x / q, i = blockIdx.x % q;
+    const uint64_t q = grid / nr, r = blockIdx.x / q, i = blockIdx.x % q;
     auto cum = [&](uint64_t k) { return k * 5 * (nr - 1) - k * (k - 1); };  // weights 5 (R - 1) - 2 r
     const uint64_t cs = cum(nr);
     split(ev(ng * cum(r) / cs), r + 1 == nr ? ng : ev(ng * cum(r + 1) / cs), q, i);
-  } else if (N == 1024 && many && nr == 4 && (gridDim.x & 3) == 0) {
+  } else if (N == 1024 && many && nr == 4 && (grid & 3) == 0) {
     // shares 22 / 18 / 14 / 10 of 64 for ranks 0..3 (linear, 2.2:1; 22 / 17 / 14 / 11 before
     // the pair granularity: a 262,144-frame batch's 17 / 64 is 8.5 pairs per workgroup)
     constexpr uint64_t c1 = 22, c2 = c1 + 18, c3 = c2 + 14, cs = c3 + 10;
-    const uint64_t q = gridDim.x / 4, r = blockIdx.x / q, i = blockIdx.x % q;
+    const uint64_t q = grid / 4, r = blockIdx.x / q, i = blockIdx.x % q;
     const uint64_t ca = r == 0 ? 0 : r == 1 ? c1 : r == 2 ? c2 : c3, cb = r == 0 ? c1 : r == 1 ? c2 : r == 2 ? c3 : cs;
     split(ev(ng * ca / cs), r == 3 ? ng : ev(ng * cb / cs), q, i);
-  } else if (ng >= 2 * (uint64_t)gridDim.x) {
+  } else if (ng >= 2 * (uint64_t)grid) {
     // equal shares in pairs over every workgroup, with few groups each too: ceil(ng / grid) groups
     // per workgroup left the last workgroups idle -- C2's 65,536 frames at N = 512 (3.2 groups per
     // workgroup) ran 4 busy workgroups of 5 per CU, and 65,536 frames at N = 2048 (5.3) left 85 of
     // 768 idle and some CUs 18 groups against 16: -11 % and -14 % per launch, outputs identical
-    split(0, ng, gridDim.x, blockIdx.x);
+    split(0, ng, grid, blockIdx.x);
   } else {
-    const uint64_t per = (ng + gridDim.x - 1) / gridDim.x;
+    const uint64_t per = (ng + grid - 1) / grid;
     g0 = (uint64_t)blockIdx.x * per;
     g0 = g0 < ng ? g0 : ng;
     g1 = g0 + per < ng ? g0 + per : ng;
@@ -1979,9 +2004,51 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   auto load = [&](float (&xv)[CH], uint64_t b, int j) {
     const GF xin = frame_ptr(b, j);
 #pragma unroll
-    for (int c = 0; c < CH; ++c) xv[c] = ld_frame<CHAIN>(xin + (c * 64 + (unsigned)lane));
+    for (int c = 0; c < CH; ++c) xv[c] = ld_frame<CHAIN || MGX_NT_FRAMES>(xin + (c * 64 + (unsigned)lane));
   };
 
+  // The workgroup's LDS tables, from the plan's image (lds_image_kernel) in one pass of 16-byte loads,
+  // issued before the first frame's: a one-frame launch (the real-time path) waits for one round trip of
+  // table loads, behind which its frame's loads are already in flight, instead of a chain of them.
+  constexpr int kImgK = 4;  // chunks per thread in the first pass (16 KB: every plan's image at N <= 2048)
+  const auto img = gbl(static_cast<const u32x4*>(img_p));
+  u32x4* const limg = reinterpret_cast<u32x4*>(smem + LY::kc_off + 128);
+  u32x4 iv[kImgK];
+#pragma unroll
+  for (int k = 0; k < kImgK; ++k) {
+    const uint32_t i = (uint32_t)threadIdx.x + k * kThreads;
+    iv[k] = img[i < nimg ? i : nimg - 1];
+  }
+  float wreg[CH];
+  if constexpr (G::WIN_REG) {
+    const GF w = gbl(win_p);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) wreg[c] = w[c * 64 + lane];
+  }
+  float xn[G::PREFETCH ? CH : 1];
+  if constexpr (G::PREFETCH) {  // (load(xn, b0, 0) with the burst's frame pointer)
+    const uint64_t f = b0 * FPW < nf ? b0 * FPW : nf - 1;
+    const GF xin = (GF)uniform_ptr(gbl(frames_p) + f * (uint64_t)N);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN || MGX_NT_FRAMES>(xin + (c * 64 + (unsigned)lane));
+  }
+  // the 13 scalar output pointers (per launch), then the image's chunks
+  if (threadIdx.x < MGX_NUM_SCALARS) reinterpret_cast<void**>(smem + LY::kc_off)[threadIdx.x] = ap->out.scalars[threadIdx.x];
+#pragma unroll
+  for (int k = 0; k < kImgK; ++k) {
+    const uint32_t i = (uint32_t)threadIdx.x + k * kThreads;
+    if (i < nimg) limg[i] = iv[k];
+  }
+  for (uint32_t i = (uint32_t)threadIdx.x + kImgK * kThreads; i < nimg; i += kThreads) limg[i] = img[i];
+  lds_barrier();
+#if MGX_WAVE_TIMES
+  const unsigned long long wt1 = wall_clock64();
+  MGX_STAMP(1);
+#endif
+
+  KlTab<N> kl;  // spectrum bin held by each register after the last pass
+#pragma unroll
+  for (int r = 0; r < R; ++r) kl.set(r, pa(kraw[r]));
   // the band lane's prefix-row offsets pd(lim[b]) | pd(lim[b + 1]) << 16 (G::BLIM_REG)
   uint32_t blim = 0;
   if constexpr (G::BLIM_REG) {
@@ -1989,14 +2056,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     const int lb = lane < kBark ? lane : 0;
     blim = (uint32_t)(kl[lb] >> 3) | ((uint32_t)(kl[lb + 1] >> 3) << 16);
   }
-  float wreg[CH];
-  if constexpr (G::WIN_REG) {
-    const GF w = gbl(ap->t.window);
-#pragma unroll
-    for (int c = 0; c < CH; ++c) wreg[c] = w[c * 64 + lane];
-  }
-  float xn[G::PREFETCH ? CH : 1];
-  if constexpr (G::PREFETCH) load(xn, b0, 0);
 
   MGX_STAMP(2);
   int it = 0;  // the wave's batch count (CHAIN with paired batches: the pair's second when odd)
@@ -2329,7 +2388,41 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
   return launch_n<N, true, false>(a, grid, stream);
 }
 
+template <int N>
+size_t lds_image_bytes_n(int ncoef, int nfilt) {
+  return (Lds<N>::bytes(ncoef, nfilt) - (Lds<N>::kc_off + 128) + 15) / 16 * 16;
+}
+
+template <int N>
+hipError_t launch_image_n(int precision, int mode, const KernelArgs& a, void* image, hipStream_t stream) {
+  auto* im = static_cast<unsigned char*>(image);
+  if (mode == MGX_MODE_LITERAL) hipLaunchKernelGGL((lds_image_kernel<N, true, true>), dim3(1), dim3(kThreads), 0, stream, a, im);
+  else if (precision == MGX_PRECISION_FAST) hipLaunchKernelGGL((lds_image_kernel<N, false, false>), dim3(1), dim3(kThreads), 0, stream, a, im);
+  else hipLaunchKernelGGL((lds_image_kernel<N, true, false>), dim3(1), dim3(kThreads), 0, stream, a, im);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+size_t lds_image_bytes(int n, int ncoef, int nfilt) {
+  switch (n) {
+    case 256: return lds_image_bytes_n<256>(ncoef, nfilt);
+    case 512: return lds_image_bytes_n<512>(ncoef, nfilt);
+    case 1024: return lds_image_bytes_n<1024>(ncoef, nfilt);
+    case 2048: return lds_image_bytes_n<2048>(ncoef, nfilt);
+    default: return 0;
+  }
+}
+
+hipError_t launch_lds_image(int n, int precision, int mode, const KernelArgs& a, void* image, hipStream_t stream) {
+  switch (n) {
+    case 256: return launch_image_n<256>(precision, mode, a, image, stream);
+    case 512: return launch_image_n<512>(precision, mode, a, image, stream);
+    case 1024: return launch_image_n<1024>(precision, mode, a, image, stream);
+    case 2048: return launch_image_n<2048>(precision, mode, a, image, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 size_t extract_lds_bytes(int n, int ncoef, int nfilt, bool chain) {
   switch (n) {

@@ -48,6 +48,11 @@ struct DevTables {
   // MGX_FLAG_MFCC_REFERENCE (plan.cpp chain_schedule, kernels.hip mel_chains):
   const uint32_t* chain_ctl; // per 8-step group and lane: row offset, chain start, the finished chain's store
   const double* chain_w;     // per track, the weights of its chains' steps back to back
+  // The workgroup's LDS tables as one image (kernels.hip lds_image_kernel, built once per plan): the bark
+  // limits' prefix-row offsets, the staged twiddles and the DCT table, byte for byte as they sit in LDS
+  // from Lds<N>::kc_off + 128 on; each launch's prologue copies it in one pass of 16-byte loads.
+  const void* lds_image;
+  uint32_t lds_image_chunks; // 16-byte chunks of the image
 };
 
 struct KernelArgs {
@@ -110,6 +115,8 @@ struct UnpackArgs {
 };
 hipError_t launch_unpack(const UnpackArgs& a, hipStream_t stream);
 size_t extract_lds_bytes(int n, int ncoef, int nfilt, bool chain);
+size_t lds_image_bytes(int n, int ncoef, int nfilt);  // DevTables::lds_image, a multiple of 16
+hipError_t launch_lds_image(int n, int precision, int mode, const KernelArgs& a, void* image, hipStream_t stream);
 int frames_per_batch(int n);
 int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt, bool chain);  // resident workgroups per CU
 

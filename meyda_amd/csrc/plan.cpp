@@ -448,6 +448,7 @@ struct mgx_plan {
   mgx_plan_desc d;
   int n = 0, L = 0;
   unsigned char* dev = nullptr;
+  void* lds_image = nullptr;  // DevTables::lds_image (its own allocation)
   mgx::DevTables t{};
   double freq_sum = 0, pow_freq_sum = 0, nyq = 0, sharp_tail = 0;
   int grid_cap = 1;
@@ -668,6 +669,26 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->t.dct = reinterpret_cast<const float*>(b + o_dct);
   p->t.chain_ctl = reinterpret_cast<const uint32_t*>(b + o_cl);
   p->t.chain_w = reinterpret_cast<const double*>(b + o_cw);
+  // the workgroup's LDS tables as one image (kernels.hip lds_image_kernel), built here once
+  {
+    const size_t ib = mgx::lds_image_bytes(n, nc, nf);
+    mgx::KernelArgs ia{};
+    ia.t = p->t;
+    ia.nfilt = nf;
+    ia.ncoef = nc;
+    e = hipMalloc(&p->lds_image, ib);
+    if (e == hipSuccess) e = hipMemset(p->lds_image, 0, ib);
+    if (e == hipSuccess) e = mgx::launch_lds_image(n, (int)d->precision, (int)d->mode, ia, p->lds_image, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) {
+      if (p->lds_image) (void)hipFree(p->lds_image);
+      (void)hipFree(p->dev);
+      delete p;
+      return hip_fail(e, "plan LDS image");
+    }
+    p->t.lds_image = p->lds_image;
+    p->t.lds_image_chunks = (uint32_t)(ib / 16);
+  }
   *out = p;
   return MGX_OK;
 }
@@ -681,6 +702,7 @@ int mgx_plan_destroy(mgx_plan* p) {
   if (p->s_comp) (void)hipStreamSynchronize(p->s_comp);
   for (auto& r : p->chain_rings) (void)hipEventSynchronize(r.done);
   if (p->dev) (void)hipFree(p->dev);
+  if (p->lds_image) (void)hipFree(p->lds_image);
   for (auto& r : p->chain_rings) {
     (void)hipEventDestroy(r.done);
     if (r.scal) (void)hipFree(r.scal);

@@ -8,7 +8,8 @@
 //   stream: start(features) then process() buffer by buffer with the callback
 //       (src/meyda.js:69-91,233-241), options.batchFrames 1 (a launch per buffer, the callback
 //       inside process()) and 64 (64 buffers per launch, callbacks in order; stop() flushes):
-//       us per buffer and buffers/s, for C1's features at N = 512 and every feature at N = 1024.
+//       the median us per launch (each launch's K process() calls timed on their own), per buffer and
+//       buffers/s, for C1's features at N = 512 and every feature at N = 1024.
 // Prints one JSON line. Needs a GPU; reads only the product and tests/golden (data).
 const fs = require('fs');
 const os = require('os');
@@ -60,30 +61,40 @@ function c1() {
     rms: r.rms, spectralCentroid: r.spectralCentroid };
 }
 
-function stream(n, feats, K, buffers) {
+function stream(n, feats, K, launches) {
   const g = goldenInputs(n);
   const frames = [];
   for (let i = 0; i < g.F; i++) frames.push(g.x.slice(i * n, (i + 1) * n));
   let got = 0;
   const m = new Meyda(ctx, null, n, () => { got++; }, { batchFrames: K });
   m.start(feats);
-  for (let i = 0; i < 4 * K; i++) m.process(frames[i % frames.length]);  // plans, JIT, staging
+  for (let i = 0; i < 50 * K; i++) m.process(frames[i % frames.length]);  // plans, JIT, staging
   m.stop();
   m.start(feats);
   got = 0;
+  // each launch's K process() calls timed on their own (the K-th launches and delivers the batch): the
+  // median per launch, robust to a GC pause or a descheduled host thread, and the mean over all of them
+  const t = [];
+  let i = 0;
   const t0 = now();
-  for (let i = 0; i < buffers; i++) m.process(frames[i % frames.length]);
-  m.stop();  // flushes the last partial batch
+  while (t.length < launches || us(t0, now()) < 1e6) {
+    const a = now();
+    for (let k = 0; k < K; k++, i++) m.process(frames[i % frames.length]);
+    t.push(us(a, now()));
+  }
   const el = us(t0, now());
+  m.stop();
   m.dispose();
-  if (got !== buffers) throw new Error('callbacks ' + got + ' != buffers ' + buffers);
-  return { bufferSize: n, batchFrames: K, features: feats, buffers, us_per_buffer: el / buffers,
-    buffers_per_s: buffers / (el * 1e-6), us_per_launch: el / Math.ceil(buffers / K) };
+  if (got !== i) throw new Error('callbacks ' + got + ' != buffers ' + i);
+  const med = pct(t, 0.5);
+  return { bufferSize: n, batchFrames: K, features: feats, buffers: i, launches: t.length, us_per_launch: med,
+    us_per_buffer: med / K, buffers_per_s: K / (med * 1e-6), us_per_launch_p90: pct(t, 0.9),
+    us_per_launch_mean: el / t.length };
 }
 
 const out = { c1: c1(), stream: [] };
 for (const [n, feats] of [[512, ['rms', 'spectralCentroid']], [1024, ALL]]) {
-  for (const K of [1, 64]) out.stream.push(stream(n, feats, K, K === 1 ? 2000 : 64 * 60));
+  for (const K of [1, 64]) out.stream.push(stream(n, feats, K, K === 1 ? 2000 : 300));
 }
 out.node = process.version;
 out.cpu_model = os.cpus()[0].model;
