@@ -299,7 +299,7 @@ def pipelined(step, devs, first, count):
     streams and two output sets (step(k) launches step k on stream k & 1 of every local
     device): a stream of batches the way a streaming caller runs it, so step i+1's workgroups
     start on the CUs step i's last waves leave while it drains (one launch ends with ~45 us of
-    SIMDs running out of waves; DESIGN.md §6.3). Forks from and joins back into stream 0."""
+    SIMDs running out of waves; DESIGN.md §4.4). Forks from and joins back into stream 0."""
     for d in devs.devs:
         e = torch.cuda.Event()
         e.record(devs.stream(d, 0))

@@ -124,7 +124,7 @@ typedef struct mgx_plan_desc {
                                         over its bins in ascending order into a float32 accumulator of
                                         double products, Math.log in double, the sequential DCT (MFCC
                                         bit-identical wherever the power spectrum is; slower, see
-                                        DESIGN.md §4.3). Default off: segmented-scan mel sums, float32
+                                        DESIGN.md §5.3). Default off: segmented-scan mel sums, float32
                                         hardware log, the matrix-core DCT, all within 1e-5. */
 
 typedef struct mgx_plan mgx_plan;

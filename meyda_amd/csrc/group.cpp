@@ -1,4 +1,4 @@
-// Multi-device groups (include/meyda_gpu.h, "Multi-device groups"; DESIGN.md §7).
+// Multi-device groups (include/meyda_gpu.h, "Multi-device groups"; DESIGN.md §10).
 //
 // Buffers are independent in the reference (src/meyda.js:69-91 keeps no state from one
 // buffer to the next), so a batch is cut into contiguous shards, one per device. Each
@@ -698,11 +698,11 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
   }
   for (size_t i = 0; i < g->m.size(); ++i)
     if (counts[g->m[i].rank] && !frames[i]) return fail(MGX_E_INVALID_ARGUMENT, "frames of local rank %zu are NULL", i);
-  // pipeline depth: about 32 Ki frames per chunk, at most 8 chunks (DESIGN.md §7). Each peer's
+  // pipeline depth: about 32 Ki frames per chunk, at most 8 chunks (DESIGN.md §10). Each peer's
   // records cross one xGMI link to the root (200 B per frame: ~52 MB per 262,144-frame shard,
   // of the order of the shard's extraction time), so what is not overlapped is about one
   // chunk's transfer after the last extraction: 8 chunks halve that tail against 4, and the
-  // chunks' kernel boundaries cost nothing on two alternating streams (DESIGN.md §7).
+  // chunks' kernel boundaries cost nothing on two alternating streams (DESIGN.md §10).
   // (a one-rank group has nothing to overlap: one chunk)
   if (nch == 0) nch = R == 1 ? 1 : (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, (most + 32767) / 32768));
   uint64_t cmax = 0;
@@ -735,7 +735,7 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
   // Consecutive chunks alternate between that stream and the member's second compute stream:
   // the chunks are independent, so chunk c+1's workgroups take the slots chunk c's free while
   // it drains instead of starting after its last workgroup. 8 chunks of 262,144 x 1024 on one
-  // stream took 9 % longer than one launch; alternating, 1 % less (DESIGN.md §7). Chunk c and
+  // stream took 9 % longer than one launch; alternating, 1 % less (DESIGN.md §10). Chunk c and
   // c+2 share a transfer slot and a stream, so the slot's reuse stays ordered on that stream.
   for (size_t i = 0; i < g->m.size(); ++i) cs.push_back(streams ? static_cast<hipStream_t>(streams[i]) : g->m[i].s_comp);
   for (size_t i = 0; i < g->m.size(); ++i) {

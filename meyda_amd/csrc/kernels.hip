@@ -24,7 +24,7 @@
 //                               contraction, on the FP64 matrix cores (v_mfma_f64_4x4x4_4b:
 //                               16 coefficients x the batch's 4 frames per instruction);
 //                               MGX_FLAG_DCT_SEQUENTIAL keeps the reference's sequential
-//                               VALU order instead (DESIGN.md §4.2)
+//                               VALU order instead (DESIGN.md §5.2)
 //    scalar features            spectral*.js, perceptual*.js
 //
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit.
@@ -251,7 +251,7 @@ __device__ __forceinline__ int pd(int d) { return d + (d >> 4); }
 // regions: 1 the FFT exchanges, 2 the amplitude row's LDS round trip, 4 phase 2, 8 the
 // per-frame reductions (moment transpose, prefix and rolloff, band sums, mel scan), 16 the
 // frame start (energy/zcr, window, stage 0), 32 the amplitude, 64 the moment partials.
-// Measured (interleaved A/B, all features): 1 alone 0.5-1 % faster than none;
+// Measured (interleaved A/B, all features; profiles/design_history_r01_r04.md): 1 alone 0.5-1 % faster than none;
 // 111 (all but the frame start, level 2) another 5.0 % at N = 1024, 4.3 % at 2048, 7.4 % at 512;
 // then levels: the exchanges and phase 2 at 3, the frame start at 1 (above the FFT's register
 // passes at 0), 127: another 1.4 % at 1024, 2.5 % at 2048, 2.1 % at 512.
@@ -288,7 +288,7 @@ struct KlTab {
 // made no change where the kernel is VALU-bound.
 // NT: a non-temporal load (the CHAIN kernels' frames: the power-row ring keeps more of the L2;
 // -0.6..-1.2 % per reference-order launch, profiles/r03_mfcc_tracks.txt. The other kernels keep
-// plain loads: C2's batch stays in the MALL between launches, which nt loads lose)
+// plain loads: C2's batch stays in the MALL between launches, which nt loads lose; profiles/r05_prologue_ab.txt)
 // A spectrum output element (amplitude, power, complex: 2-8 KB per frame, written once and never
 // read back): a non-temporal store, which streams past the caches instead of filling them (every
 // output at N = 1024: -8.1..-8.8 % per launch; C2's 1 GiB batch -0.7 %, outputs identical; the same
@@ -882,7 +882,7 @@ __device__ __forceinline__ int dpp_i(int v) {
 // belongs to one segment, and band j = (rising half on segment j) + (falling half on
 // segment j+1). So E_j = U_j + D_{j+1} with U_m = sum_{k in m} up(k) p_k and
 // D_m = sum_{k in m} dn(k) p_k: two segmented sums over the bins, computed as in-lane
-// runs plus one segmented scan across the lanes (DESIGN.md §4.3). Where the segments start
+// runs plus one segmented scan across the lanes (DESIGN.md §5.1). Where the segments start
 // does not depend on the frame, so every branch of that logic is a plan table
 // (plan.cpp mel_lane_tables): per bin a keep factor (0 restarts the sums) and the scratch
 // slot the running sums are stored to, per lane the keeps of the six scan steps and the two
@@ -919,7 +919,7 @@ struct MelTab {
 // belongs to one segment, and band j = (rising half on segment j) + (falling half on
 // segment j+1). So E_j = U_j + D_{j+1} with U_m = sum_{k in m} up(k) p_k and
 // D_m = sum_{k in m} dn(k) p_k: two segmented sums over the bins, computed as in-lane
-// runs plus one segmented scan across the lanes (DESIGN.md §4.3). Where the segments start
+// runs plus one segmented scan across the lanes (DESIGN.md §5.1). Where the segments start
 // does not depend on the frame, so every branch of that logic is a plan table (MelTab,
 // plan.cpp mel_lane_tables): per bin the weight pair and a keep factor (0 restarts the sums),
 // per lane the keeps of the six scan steps and, per band, where its two segment totals end up.
@@ -1765,7 +1765,7 @@ __device__ __forceinline__ void mfcc_dct(KArgs* q, int l2, FrameRec* recs, const
   if (CHAIN || q->dct_sequential) {
     // MGX_FLAG_DCT_SEQUENTIAL, and the reference-order MFCC (CHAIN): VALU FMAs in the reference's
     // sequential order, one lane per (coefficient, frame). (The matrix-core form below is the
-    // default: 0.5 % faster for the whole kernel and equal on every golden coefficient; DESIGN.md §4.2.)
+    // default: 0.5 % faster for the whole kernel and equal on every golden coefficient; DESIGN.md §5.2.)
     for (int i = l2; i < FPW * nc; i += 64) {
       const int c = (int)((unsigned)i / FPW), fb = i & (FPW - 1);
       const uint64_t f = fbase + fb;

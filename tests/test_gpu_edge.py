@@ -34,7 +34,7 @@ def compare(out, ref, n, sr=44100.0, spectra_exact_min=None):
     # the reference's full complex FFT forms 0 * Inf in its j = 0 twiddle product, which
     # turns the imaginary companion of the real DC / X[N/4] values into NaN; the
     # half-spectrum network never forms that product, so those two bins can be +-Inf where
-    # the reference has NaN (DESIGN.md §8). Every other bin, and every feature (checked
+    # the reference has NaN (DESIGN.md §6). Every other bin, and every feature (checked
     # above), matches in class.
     nonfin = ~np.isfinite(r).all(1)
     ex = np.zeros(a.shape, bool)
