@@ -117,7 +117,10 @@ struct Geo {
   // this frame, after the last table loads this frame waits on (twiddles: the passes are
   // done; the mel records: issued just before), so no wait of this frame is held up by
   // it; PF = 0 loads each frame when its wave starts it.
-  static constexpr int PF = N <= 256 ? 1 : N <= 1024 ? 2 : 0;  // measured best per N
+#ifndef MGX_PF_2048
+#define MGX_PF_2048 0
+#endif
+  static constexpr int PF = N <= 256 ? 1 : N <= 1024 ? 2 : MGX_PF_2048;  // measured best per N
   // WIN_REG: the window held in registers for the whole launch (CH VGPRs) instead of loaded
   // per frame (N = 1024, where the LDS twiddles freed the registers: 1.1-1.5 % faster, 119
   // VGPRs; the frame prefetch at the frame's start instead, PF = 1, 0.9-1.1 %, and both
@@ -317,12 +320,13 @@ __device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))
 #endif
 
 // Phase stamps of the diagnostic build (-DMGX_WAVE_TIMES=1 only; tools/small_stamps.py): the 100 MHz
-// real-time clock at MGX_STAMP(i), written by the first lane of the first workgroup.
+// real-time clock at MGX_STAMP(i), written by the first lane of a one-workgroup launch (a small host
+// batch; in a large launch the stamps would slow its first wave at every frame).
 #if MGX_WAVE_TIMES
 __device__ unsigned long long g_stamps[16];
 #define MGX_STAMP(i)                                                                              \
   do {                                                                                            \
-    if (blockIdx.x == 0 && threadIdx.x == 0) ((volatile unsigned long long*)g_stamps)[i] = wall_clock64(); \
+    if (gridDim.x == 1 && threadIdx.x == 0) ((volatile unsigned long long*)g_stamps)[i] = wall_clock64(); \
   } while (0)
 #else
 #define MGX_STAMP(i) ((void)0)
@@ -331,7 +335,7 @@ __device__ unsigned long long g_stamps[16];
 #if MGX_WAVE_TIMES
 #define MGX_CLOCK_STAMP(i)                                                                        \
   do {                                                                                            \
-    if (blockIdx.x == 0 && threadIdx.x == 0) ((volatile unsigned long long*)g_stamps)[i] = clock64(); \
+    if (gridDim.x == 1 && threadIdx.x == 0) ((volatile unsigned long long*)g_stamps)[i] = clock64(); \
   } while (0)
 #else
 #define MGX_CLOCK_STAMP(i) ((void)0)

@@ -67,14 +67,20 @@ def main():
         print("XCD %d (wg %% 8): waves %d  end mean %.1f  min %.1f  max %.1f us" % (k, m.sum(), us(t2[m]).mean(), us(t2[m]).min(), us(t2[m]).max()))
     # which waves finish first: by workgroup rank groups and by the wave's index in its workgroup
     ng = len(np.unique(wg))
-    for name, key in (("wg // (grid/4)", wg // max(1, ng // 4)), ("wg % 4", wg % 4), ("wave in wg", np.arange(len(wg)) % 4)):
+    ranks = max(1, ng // 256)  # workgroups per CU of the persistent grid (256 CUs): rank = wg // (grid / ranks)
+    for name, key in (("rank wg//(grid/%d)" % ranks, wg // max(1, ng // ranks)), ("wave in wg", np.arange(len(wg)) % 4)):
         print("end by %-15s: %s" % (name, "  ".join("%d:%.0f" % (k, us(t2[key == k]).mean()) for k in np.unique(key)[:8])))
+    rk = wg // max(1, ng // ranks)
+    for k in np.unique(rk):
+        q = np.percentile(us(t2[rk == k]), [0, 10, 50, 90, 100])
+        print("rank %d end pct 0/10/50/90/100: %s us" % (k, " ".join("%.0f" % z for z in q)))
     # resident waves over time: what fraction of the 16 slots per CU x 256 CUs is alive
     grid = np.linspace(0, span, 41)
     alive = [((us(t0) <= g) & (us(t2) > g)).sum() for g in grid]
     print("alive waves over the launch (41 samples):", " ".join(str(v) for v in alive))
     area = np.sum((t2 - t0) / 100.0)
-    print("mean resident waves %.1f of 4096 slots (%.3f)" % (area / span, area / span / 4096))
+    slots = 1024 * ranks
+    print("mean resident waves %.1f of %d slots (%.3f)" % (area / span, slots, area / span / slots))
 
 
 if __name__ == "__main__":
