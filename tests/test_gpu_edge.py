@@ -135,6 +135,26 @@ def test_mel_band_counts(capi, oracle_mod, nmel):
     assert not tolerance.check_vectors(out["mfcc"], ref["mfcc"]), nmel
 
 
+@pytest.mark.parametrize("flags", [{}, {"dct_sequential": True}, {"mfcc_reference": True}])
+def test_largest_lds_image(capi, oracle_mod, flags):
+    """64 mel bands x 32 coefficients at N = 1024: the plan's LDS image (bark limits, twiddles, DCT table;
+    kernels.hip lds_image_kernel) is larger than the prologue's first pass of 16-byte loads, so its tail
+    (the DCT rows past 16 KB) takes the second loop. Every output but the MFCC equals the 13-coefficient
+    plan's bit for bit (the twiddles came through), and each of the first 13 coefficients is that plan's
+    DCT sum over 32 instead of 13 (mfcc.js:91; the reference fixes numCoeffs = 13, the engine allows 1..32)."""
+    n = 1024
+    x = oracle_mod.synth_frames(0x6D657964, 301, 40, n)
+    a = capi.Plan(buffer_size=n, num_mel_bands=64, num_mfcc_coeffs=32, scalar_f64=True, **flags).extract(x, FEATS)
+    b = capi.Plan(buffer_size=n, num_mel_bands=64, scalar_f64=True, **flags).extract(x, FEATS)
+    for k in b:
+        if k != "mfcc":
+            assert np.array_equal(a[k], b[k], equal_nan=True), k
+    v32 = a["mfcc"].reshape(len(x), 32)[:, :13].astype(np.float64) * 32
+    v13 = b["mfcc"].reshape(len(x), 13).astype(np.float64) * 13
+    scale = np.abs(v13).max(axis=1, keepdims=True)
+    assert (np.abs(v32 - v13) <= 1e-6 * scale).all()
+
+
 def test_n256_batch(capi, oracle_mod):
     n = 256
     x = oracle_mod.synth_frames(0x6D657964, 9, 200, n)
