@@ -1339,6 +1339,21 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
       st_out(&o[c * 64 + (unsigned)lane], av * av);  // powerSpectrum.js
     }
   }
+  if constexpr (CHAIN) {
+    // the frame's power row (powerSpectrum.js) for the mel chains in phase 2 (mel_chains): ring slot fb, or
+    // with paired batches 4 (it & 1) + fb. Stored here from the amplitude row in LDS, lane l of store c
+    // writing bin 64 c + l: 256 contiguous bytes per store, where the lane's own bins [R l, R l + R) were
+    // R 4-byte stores 4 R bytes apart; profiles/r05_chain_rows.txt).
+    // A non-finite frame's slot then takes its mel sums instead (below).
+    if (ap->need_mfcc) {
+      auto row = gbl(rows) + ((ap->chain_pair ? 4 * (it & 1) : 0) + fb) * L;
+#pragma unroll
+      for (int c = 0; c < R; ++c) {
+        const float a = amp[pa(c * 64 + lane)];
+        row[c * 64 + (unsigned)lane] = a * a;
+      }
+    }
+  }
 
   // Per-frame reductions, lane t owns bins [R t, R t + R).
   float av[R];
@@ -1544,21 +1559,15 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
     mel_energies<N>(ap, av, lane, buf, rec, mt);
   }
   if constexpr (CHAIN) {
-    // the frame's power row (powerSpectrum.js) for the mel chains in phase 2 (mel_chains): ring slot
-    // fb, or with paired batches 4 (it & 1) + fb. A non-finite frame keeps the mel sums
-    // nonfinite_frame_sums formed (its flag: lm[31] of its half, or a bit of its zcr count): they go
-    // to the start of its ring slot instead, and mel_chains puts them back after its chains
-    // (whose stores do not look at the flag).
+    // A non-finite frame keeps the mel sums nonfinite_frame_sums formed (its flag: lm[31] of its half, or a
+    // bit of its zcr count): they go to the start of its ring slot, over its power row, and mel_chains puts
+    // them back after its chains (whose stores do not look at the flag).
     if (ap->need_mfcc) {
       const bool pair = ap->chain_pair;
-      // (the wave's ring in device memory: R consecutive floats per lane)
       auto row = gbl(rows) + ((pair ? 4 * (it & 1) : 0) + fb) * L;
-      if (nonfinite) {
+      if (nonfinite) {  // (over the power row stored above)
         wave_sync();
         if (lane < ap->nfilt) row[lane] = rec.lm[(pair && !(it & 1) ? 32 : 0) + lane];
-      } else {
-#pragma unroll
-        for (int jj = 0; jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];
       }
       if (pair) {
         if (lane == 0) rec.lm[(it & 1 ? 0 : 32) + 31] = nonfinite ? 1.0f : 0.0f;

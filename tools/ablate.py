@@ -49,9 +49,9 @@ PATCHES = {
     # power-row cost alone)
     "chain_none": [("        if (q->chain_pair) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);",
                     "        if (opaque(0)) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);")],
-    # the chains' weight and row loads replaced by values from the control word (no loads)
-    "chain_norows": [("      for (int jj = 0; jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];",
-                      "      for (int jj = 0; opaque(0) && jj < R; ++jj) row[R * lane + jj] = av[jj] * av[jj];")],
+    # the power-row stores skipped (the chains read stale rows)
+    "chain_norows": [("      for (int c = 0; c < R; ++c) {\n        const float a = amp[pa(c * 64 + lane)];",
+                      "      for (int c = 0; opaque(0) && c < R; ++c) {\n        const float a = amp[pa(c * 64 + lane)];")],
     # the fence before the chains (a vmcnt(0) wait: the next frame's prefetch, the row stores) dropped
     "chain_nofence": [("""        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
