@@ -28,6 +28,9 @@
 //    scalar features            spectral*.js, perceptual*.js
 //
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit.
+#include <cstring>
+#include <type_traits>
+
 #include "mgx_internal.h"
 
 namespace mgx {
@@ -810,6 +813,12 @@ __device__ __forceinline__ KArgs* args_ptr() {
   KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(p));
   return p;
+}
+
+// KernelArgsInline::frame of a one-frame launch that carries its frame in the kernel arguments (INL)
+__device__ __forceinline__ const float* inline_frame_ptr() {
+  const auto q = (const __attribute__((address_space(4))) KernelArgsInline*)args_ptr();
+  return (const float*)q->frame;
 }
 
 // Pointers read through args_ptr() are generic; re-type them as global (address space 1)
@@ -1895,8 +1904,9 @@ __device__ __forceinline__ void done_signal(KArgs* q, int lane) {
 __device__ unsigned long long g_wave_times[65536 * 4];
 #endif
 
-template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(KernelArgs a) {
+template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN, bool INL = false>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(
+    std::conditional_t<INL, KernelArgsInline, KernelArgs> a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   using LY = Lds<N>;
@@ -1919,16 +1929,36 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   MGX_STAMP(0);
   MGX_CLOCK_STAMP(13);
 #endif
+  // The 13 scalar output pointers (per launch) as the first load: its address needs nothing but the kernarg
+  // pointer, and issued first its wait (vmcnt, in issue order) holds for no later load
+  void* kp = nullptr;
+  if (threadIdx.x < MGX_NUM_SCALARS) kp = ap->out.scalars[threadIdx.x];
+  // INL (a one-frame launch with its frame in the kernel arguments): the frame's loads next, from the
+  // kernarg segment the wave addresses from its start, so they overlap every wait below
+  float xn[G::PREFETCH ? CH : 1];
+  if constexpr (INL && G::PREFETCH) {
+    const GF xin = (GF)uniform_ptr(gbl(inline_frame_ptr()));
+#pragma unroll
+    for (int c = 0; c < CH; ++c) xn[c] = xin[c * 64 + (unsigned)lane];
+  }
   // The kernel arguments the prologue reads, loaded in one burst and waited for together (the empty asm
   // keeps their loads here, ahead of every branch): a one-frame launch (the real-time path) then pays one
   // round trip to the kernarg segment before its table and frame loads issue, not one per dependent step.
   const uint64_t nf = ap->num_frames;
   const uint32_t nr32 = (uint32_t)ap->wg_ranks, nimg = ap->t.lds_image_chunks, grid = gridDim.x;
   const void* const img_p = ap->t.lds_image;
-  const float* const frames_p = ap->frames;
+  // (INL: the launch's one frame in the kernarg segment, KernelArgsInline::frame)
+  const float* const frames_p = INL ? inline_frame_ptr() : ap->frames;
   const float* const win_p = ap->t.window;
   const int* const klist_p = ap->t.klist;
-  asm volatile("" ::"s"(nf), "s"(nr32), "s"(nimg), "s"(grid), "s"(img_p), "s"(frames_p), "s"(win_p), "s"(klist_p));
+  // ... with one word of every other 64-byte line of the arguments in the same burst, so the scalar cache
+  // holds them all: the fields read later (the feature flags, the output and table pointers, the constants)
+  // then hit instead of each costing a round trip of a one-frame launch's serial chain
+  static_assert(sizeof(KernelArgs) <= 8 * 64, "the argument lines touched below");
+  const auto kw = reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(ap);
+  const uint32_t t2 = kw[32], t3 = kw[48], t4 = kw[64], t5 = kw[80], t6 = kw[96], t7 = kw[(sizeof(KernelArgs) - 4) / 4];
+  asm volatile("" ::"s"(nf), "s"(nr32), "s"(nimg), "s"(grid), "s"(img_p), "s"(frames_p), "s"(win_p), "s"(klist_p), "s"(t2),
+               "s"(t3), "s"(t4), "s"(t5), "s"(t6), "s"(t7));
 
   int lp[G::NPASS];
 #pragma unroll
@@ -2012,7 +2042,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     uint64_t f = b * FPW + j;
     f = f < nf ? f : nf - 1;
     // (wave-uniform, uniform_ptr: the lane's offset is added at each load)
-    return (GF)uniform_ptr(gbl(args_ptr()->frames) + f * (uint64_t)N);
+    const float* base = INL ? inline_frame_ptr() : args_ptr()->frames;
+    return (GF)uniform_ptr(gbl(base) + f * (uint64_t)N);
   };
   auto load = [&](float (&xv)[CH], uint64_t b, int j) {
     const GF xin = frame_ptr(b, j);
@@ -2038,15 +2069,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
 #pragma unroll
     for (int c = 0; c < CH; ++c) wreg[c] = w[c * 64 + lane];
   }
-  float xn[G::PREFETCH ? CH : 1];
-  if constexpr (G::PREFETCH) {  // (load(xn, b0, 0) with the burst's frame pointer)
+  if constexpr (G::PREFETCH && !INL) {  // (load(xn, b0, 0) with the burst's frame pointer)
     const uint64_t f = b0 * FPW < nf ? b0 * FPW : nf - 1;
     const GF xin = (GF)uniform_ptr(gbl(frames_p) + f * (uint64_t)N);
 #pragma unroll
     for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN || MGX_NT_FRAMES>(xin + (c * 64 + (unsigned)lane));
   }
-  // the 13 scalar output pointers (per launch), then the image's chunks
-  if (threadIdx.x < MGX_NUM_SCALARS) reinterpret_cast<void**>(smem + LY::kc_off)[threadIdx.x] = ap->out.scalars[threadIdx.x];
+  // the output pointers, then the image's chunks
+  if (threadIdx.x < MGX_NUM_SCALARS) reinterpret_cast<void**>(smem + LY::kc_off)[threadIdx.x] = kp;
 #pragma unroll
   for (int k = 0; k < kImgK; ++k) {
     const uint32_t i = (uint32_t)threadIdx.x + k * kThreads;
@@ -2335,8 +2365,18 @@ __global__ void unpack_kernel(UnpackArgs a) {
 }
 
 template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false, bool CHAIN = false>
-hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream) {
+hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream, const float* inl = nullptr) {
   const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
+  if constexpr (N <= kInlineMaxN && FAITH && !LITERAL && !CHAIN) {
+    if (inl) {  // the one frame in the kernel arguments (KernelArgsInline)
+      KernelArgsInline x;
+      x.a = a;
+      memcpy(x.frame, inl, N * sizeof(float));
+      hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN, true>), dim3(grid), dim3(kThreads), lds,
+                         stream, x);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN>), dim3(grid), dim3(kThreads), lds, stream, a);
   return hipGetLastError();
 }
@@ -2376,7 +2416,7 @@ int occupancy_prec(int precision, int mode, int ncoef, int nfilt, bool chain) {
 }
 
 template <int N>
-hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, hipStream_t stream) {
+hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, hipStream_t stream, const float* inl) {
   if (mode == MGX_MODE_LITERAL) return launch_n<N, true, true>(a, grid, stream);
   if (precision == MGX_PRECISION_FAST) return launch_n<N, false, false>(a, grid, stream);
   const bool every = a.need_mom == 2 && a.need_prefix && a.need_energy && a.need_zcr;
@@ -2391,14 +2431,14 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
   // (LIGHT: a subset reading neither the moments nor the prefix row, e.g. mfcc or the spectra
   // alone, compiled without that code: no runtime branches to keep its registers live)
   if (a.need_spectrum && a.need_mom == 0 && !a.need_prefix)
-    return launch_n<N, true, false, true, true>(a, grid, stream);
+    return launch_n<N, true, false, true, true>(a, grid, stream, inl);
   // (NOTIME: every spectral sum but no rms / energy / zcr, e.g. C3: the all-feature schedule
   // with the time-domain reductions compiled out)
   if (a.need_spectrum && a.need_mom == 2 && a.need_prefix && !a.need_energy && !a.need_zcr)
-    return launch_n<N, true, false, false, false, true>(a, grid, stream);
+    return launch_n<N, true, false, false, false, true>(a, grid, stream, inl);
   if (a.need_spectrum && !every)
-    return launch_n<N, true, false, true>(a, grid, stream);
-  return launch_n<N, true, false>(a, grid, stream);
+    return launch_n<N, true, false, true>(a, grid, stream, inl);
+  return launch_n<N, true, false>(a, grid, stream, inl);
 }
 
 template <int N>
@@ -2468,12 +2508,13 @@ int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt, 
 }
 
 hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, int grid,
-                          hipStream_t stream) {
+                          hipStream_t stream, const float* inline_frame) {
+  if (a.num_frames != 1) inline_frame = nullptr;
   switch (n) {
-    case 256: return launch_prec<256>(precision, mode, a, grid, stream);
-    case 512: return launch_prec<512>(precision, mode, a, grid, stream);
-    case 1024: return launch_prec<1024>(precision, mode, a, grid, stream);
-    case 2048: return launch_prec<2048>(precision, mode, a, grid, stream);
+    case 256: return launch_prec<256>(precision, mode, a, grid, stream, inline_frame);
+    case 512: return launch_prec<512>(precision, mode, a, grid, stream, inline_frame);
+    case 1024: return launch_prec<1024>(precision, mode, a, grid, stream, nullptr);
+    case 2048: return launch_prec<2048>(precision, mode, a, grid, stream, nullptr);
     default: return hipErrorInvalidValue;
   }
 }

@@ -92,13 +92,26 @@ struct KernelArgs {
   uint64_t* scal_rows;   // the scalar window: kScalWords 8-byte words per wave of the grid (kernels.hip scalar_pass)
 };
 
+// A one-frame launch at N <= kInlineMaxN (the real-time path: extract_host_small with one frame) carries
+// its frame in the kernel arguments, after the KernelArgs: the kernel's first loads read it from the
+// kernarg segment, whose address the wave holds from its first instruction, instead of waiting for the
+// arguments before it can issue the frame's read of pinned host memory over PCIe.
+constexpr int kInlineMaxN = 512;
+struct KernelArgsInline {
+  KernelArgs a;
+  alignas(16) float frame[kInlineMaxN];
+};
+
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int hip_fail(hipError_t e, const char* what);
 
 // Launchers (kernels.hip).
+// inline_frame (host memory, N floats): a one-frame launch at N <= kInlineMaxN passes its frame in the
+// kernel arguments (KernelArgsInline) when a faithful per-buffer kernel without the reference-order
+// chains runs it; a.frames is then not read. Otherwise ignored.
 hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, int grid,
-                          hipStream_t stream);
+                          hipStream_t stream, const float* inline_frame = nullptr);
 hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t first_index,
                         hipStream_t stream);
 hipError_t launch_pcm_decode(const void* pcm, uint64_t count, uint32_t format, uint32_t channels,

@@ -494,7 +494,7 @@ struct mgx_plan {
 
 namespace {
 int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o, void* stream,
-                        const uint32_t* done);
+                        const uint32_t* done, const float* inline_frame = nullptr);
 }  // namespace
 
 extern "C" {
@@ -739,9 +739,11 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
 
 namespace {
 
-// mgx_extract_device, and with `done` (the small host path) the launch's completion word
+// mgx_extract_device, and with `done` (the small host path) the launch's completion word; inline_frame
+// (the small path's one frame in host memory) goes into the kernel arguments where the kernel takes it
+// (mgx::launch_extract)
 int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o, void* stream,
-                        const uint32_t* done) {
+                        const uint32_t* done, const float* inline_frame) {
   if (!p || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL plan or outputs");
   if (nframes == 0) return MGX_OK;
   if (!frames) return fail(MGX_E_INVALID_ARGUMENT, "frames is NULL");
@@ -834,7 +836,7 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
     a.done_seq = p->done_seq;
     a.done_waves = (uint32_t)grid * 4;
   }
-  e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream);
+  e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream, inline_frame);
   if (e != hipSuccess) return hip_fail(e, "extract kernel launch");
   if (ring_done) {
     e = hipEventRecord(ring_done, (hipStream_t)stream);
@@ -990,7 +992,8 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
   }
   uint32_t* const ddone = p->d_done_map;
   p->done_seq = p->done_seq + 1 ? p->done_seq + 1 : 1;  // never 0, the word's initial value
-  rc = extract_device_impl(p, static_cast<const float*>(din), nframes, &d, p->s_comp, ddone);
+  // (one frame: also handed over in the kernel arguments, read there by the kernels that take it)
+  rc = extract_device_impl(p, static_cast<const float*>(din), nframes, &d, p->s_comp, ddone, nframes == 1 ? p->h_in : nullptr);
   if (rc) {
     (void)hipStreamSynchronize(p->s_comp);
     return rc;
