@@ -4,7 +4,9 @@
 //   B  a host spin on the mapped output words (sentinel bits -> value), then the stream sync,
 //   C  an empty kernel + hipStreamSynchronize (the launch and wake-up floor),
 //   E  a busy loop on hipStreamQuery, F  an event and a busy loop on hipEventQuery,
-//   D  the kernel's own duration between two events, G  the same on device-resident frames and outputs.
+//   D  the kernel's own duration between two events, G  the same on device-resident frames and outputs,
+//   H  a kernel that only releases a sequence number to a mapped host word, the host spinning on it (the
+//      protocol's floor), H2 the same with 2,480 bytes of kernel arguments, I  mgx_extract_host itself.
 // Build: hipcc --offload-arch=gfx950 -O2 -I include -o tools/ubench/small_latency tools/ubench/small_latency.hip \
 //          -L meyda_amd -lmeyda_gpu -Wl,-rpath,$PWD/meyda_amd
 // usage: small_latency [N] [calls]
@@ -29,6 +31,20 @@
   } while (0)
 
 __global__ void empty_kernel() {}
+// H: the floor of the small host path's protocol -- a kernel that only releases a sequence number to a
+// mapped host word (as done_signal), the host spinning on it; H2 the same with 2,480 bytes of kernel
+// arguments (KernelArgsInline's size: what a one-frame launch at N = 512 passes)
+__global__ void flag_kernel(uint32_t* flag, uint32_t seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+struct BigArgs {
+  uint32_t* flag;
+  uint32_t seq;
+  float pad[616];
+};
+__global__ void flag_kernel_big(BigArgs a) {
+  if (threadIdx.x == 0) __hip_atomic_store(a.flag, a.seq + (uint32_t)a.pad[threadIdx.x], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 static double now_us() {
   timespec t;
@@ -80,7 +96,30 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  std::vector<double> ta, tb, tc, td, tl, te, tf;
+  std::vector<double> ta, tb, tc, td, tl, te, tf, th, th2, ti;
+  uint32_t* hflag = nullptr;
+  uint32_t* dflag = nullptr;
+  CK(hipHostMalloc((void**)&hflag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  CK(hipHostGetDevicePointer((void**)&dflag, hflag, 0));
+  volatile uint32_t* vflag = hflag;
+  *vflag = 0;
+  uint32_t seq = 0;
+  BigArgs big;
+  memset(&big, 0, sizeof(big));
+  big.flag = dflag;
+  // I: the product's one-frame host call (mgx_extract_host: pinned buffers, the frame in the kernel arguments
+  // at N <= 512, the completion word) for the same two features
+  double hrms[1], hcen[1];
+  mgx_plan_desc dh;
+  mgx_plan_desc_init(&dh);
+  dh.buffer_size = (uint32_t)n;
+  dh.scalar_f64 = 1;
+  mgx_plan* ph = nullptr;
+  if (mgx_plan_create(&dh, &ph) != MGX_OK) return 1;
+  mgx_outputs oh;
+  memset(&oh, 0, sizeof(oh));
+  oh.scalars[MGX_RMS] = hrms;
+  oh.scalars[MGX_SPECTRAL_CENTROID] = hcen;
   for (int it = 0; it < calls + 50; ++it) {
     // A: launch + stream synchronise
     double t0 = now_us();
@@ -115,6 +154,23 @@ int main(int argc, char** argv) {
     empty_kernel<<<1, 64, 0, s>>>();
     CK(hipStreamSynchronize(s));
     double t6 = now_us();
+    // H / H2: the flag kernel's round trip
+    double t11 = now_us();
+    flag_kernel<<<1, 64, 0, s>>>(dflag, ++seq);
+    while (*vflag != seq) {
+    }
+    double t12 = now_us();
+    big.seq = ++seq;
+    double t13 = now_us();
+    flag_kernel_big<<<1, 64, 0, s>>>(big);
+    while (*vflag != seq) {
+    }
+    double t14 = now_us();
+    CK(hipStreamSynchronize(s));
+    // I: the product's host call
+    double t15 = now_us();
+    if (mgx_extract_host(ph, hin, 1, &oh) != MGX_OK) return 1;
+    double t16 = now_us();
     // D: kernel duration
     CK(hipEventRecord(e0, s));
     if (mgx_extract_device(p, din, 1, &o, s) != MGX_OK) return 1;
@@ -137,14 +193,18 @@ int main(int argc, char** argv) {
       td.push_back(ms * 1e3);
       te.push_back(t8 - t7);
       tf.push_back(t10 - t9);
+      th.push_back(t12 - t11);
+      th2.push_back(t14 - t13);
+      ti.push_back(t16 - t15);
     }
   }
   printf("{\"n\": %d, \"calls\": %d, \"launch_sync_us\": %.2f, \"launch_call_us\": %.2f, \"launch_spin_us\": %.2f, "
          "\"launch_stream_query_us\": %.2f, \"launch_event_query_us\": %.2f, "
          "\"empty_kernel_sync_us\": %.2f, \"kernel_event_us\": %.2f, \"kernel_event_device_io_us\": %.2f, "
+         "\"flag_kernel_spin_us\": %.2f, \"flag_kernel_2480B_args_spin_us\": %.2f, \"extract_host_us\": %.2f, "
          "\"rms\": %.9g, \"centroid\": %.9g}\n",
-         n, calls, median(ta), median(tl), median(tb), median(te), median(tf), median(tc), median(td), median(tg), hout[0],
-         hout[16]);
+         n, calls, median(ta), median(tl), median(tb), median(te), median(tf), median(tc), median(td), median(tg), median(th),
+         median(th2), median(ti), hout[0], hout[16]);
   mgx_plan_destroy(p);
   return 0;
 }
