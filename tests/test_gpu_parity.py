@@ -313,6 +313,31 @@ def test_small_host_batches_equal_staged_path(capi, n):
             assert np.array_equal(a2[k].view(np.uint8), b2[k].view(np.uint8)), (F, k, "second call")
 
 
+@pytest.mark.parametrize("n", [256, 512])
+def test_one_frame_calls_with_the_frame_in_the_kernel_arguments(capi, n):
+    """A one-frame host call at N <= 512 passes its frame inside the kernel arguments (KernelArgsInline;
+    kernels.hip extract_kernel<..., INL>): each kernel kind that takes it -- every feature, a subset (SUB),
+    a light subset (LIGHT: mfcc or a spectrum alone), every spectral feature without the time-domain ones
+    (NOTIME) -- must give the device path's bits, for ordinary and for non-finite frames, call after call."""
+    import torch
+    rng = np.random.default_rng(n + 3)
+    p = capi.Plan(buffer_size=n, scalar_f64=True)
+    spectral = [f for f in capi.ALL_FEATURES if f not in ("rms", "energy", "zcr")]
+    kinds = [capi.ALL_FEATURES, ["rms", "spectralCentroid"], ["zcr", "spectralRolloff", "loudness"], ["mfcc"],
+             ["amplitudeSpectrum"], spectral]
+    for i in range(12):
+        x = rng.uniform(-1, 1, (1, n)).astype(np.float32)
+        if i % 4 == 3:
+            x[0, 5] = np.inf if i % 8 == 3 else np.nan
+        feats = kinds[i % len(kinds)]
+        a = p.extract(x, feats)
+        d = p.extract_torch(torch.from_numpy(x).cuda(), feats)
+        torch.cuda.synchronize()
+        for k in a:
+            assert np.array_equal(a[k].view(np.uint8), d[k].cpu().numpy().view(np.uint8)), (i, feats, k)
+    p.close()
+
+
 def test_small_and_staged_calls_alternate_on_one_plan(capi):
     """One plan serving small host batches (its own compute stream, created by the small path) and
     staged ones (which create the copy stream beside it) in turn, then destroyed: the staged path must

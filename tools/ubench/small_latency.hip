@@ -6,7 +6,8 @@
 //   E  a busy loop on hipStreamQuery, F  an event and a busy loop on hipEventQuery,
 //   D  the kernel's own duration between two events, G  the same on device-resident frames and outputs,
 //   H  a kernel that only releases a sequence number to a mapped host word, the host spinning on it (the
-//      protocol's floor), H2 the same with 2,480 bytes of kernel arguments, I  mgx_extract_host itself.
+//      protocol's floor), H2 the same with 2,480 bytes of kernel arguments, H3 the same through
+//      hipModuleLaunchKernel with pre-packed arguments, I  mgx_extract_host itself.
 // Build: hipcc --offload-arch=gfx950 -O2 -I include -o tools/ubench/small_latency tools/ubench/small_latency.hip \
 //          -L meyda_amd -lmeyda_gpu -Wl,-rpath,$PWD/meyda_amd
 // usage: small_latency [N] [calls]
@@ -96,12 +97,14 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  std::vector<double> ta, tb, tc, td, tl, te, tf, th, th2, ti;
+  std::vector<double> ta, tb, tc, td, tl, te, tf, th, th2, th3, ti;
   uint32_t* hflag = nullptr;
   uint32_t* dflag = nullptr;
   CK(hipHostMalloc((void**)&hflag, 64, hipHostMallocMapped | hipHostMallocCoherent));
   CK(hipHostGetDevicePointer((void**)&dflag, hflag, 0));
   volatile uint32_t* vflag = hflag;
+  hipFunction_t fk;
+  CK(hipGetFuncBySymbol(&fk, reinterpret_cast<const void*>(flag_kernel)));
   *vflag = 0;
   uint32_t seq = 0;
   BigArgs big;
@@ -167,6 +170,20 @@ int main(int argc, char** argv) {
     }
     double t14 = now_us();
     CK(hipStreamSynchronize(s));
+    // H3: the flag kernel through hipModuleLaunchKernel with the arguments pre-packed (HIP_LAUNCH_PARAM_BUFFER_*)
+    struct {
+      uint32_t* flag;
+      uint32_t seq;
+      uint32_t pad;
+    } packed = {dflag, ++seq, 0};
+    size_t psize = sizeof(packed);
+    void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &packed, HIP_LAUNCH_PARAM_BUFFER_SIZE, &psize, HIP_LAUNCH_PARAM_END};
+    double t17 = now_us();
+    CK(hipModuleLaunchKernel(fk, 1, 1, 1, 64, 1, 1, 0, s, nullptr, extra));
+    while (*vflag != seq) {
+    }
+    double t18 = now_us();
+    CK(hipStreamSynchronize(s));
     // I: the product's host call
     double t15 = now_us();
     if (mgx_extract_host(ph, hin, 1, &oh) != MGX_OK) return 1;
@@ -196,15 +213,17 @@ int main(int argc, char** argv) {
       th.push_back(t12 - t11);
       th2.push_back(t14 - t13);
       ti.push_back(t16 - t15);
+      th3.push_back(t18 - t17);
     }
   }
   printf("{\"n\": %d, \"calls\": %d, \"launch_sync_us\": %.2f, \"launch_call_us\": %.2f, \"launch_spin_us\": %.2f, "
          "\"launch_stream_query_us\": %.2f, \"launch_event_query_us\": %.2f, "
          "\"empty_kernel_sync_us\": %.2f, \"kernel_event_us\": %.2f, \"kernel_event_device_io_us\": %.2f, "
-         "\"flag_kernel_spin_us\": %.2f, \"flag_kernel_2480B_args_spin_us\": %.2f, \"extract_host_us\": %.2f, "
+         "\"flag_kernel_spin_us\": %.2f, \"flag_kernel_2480B_args_spin_us\": %.2f, \"flag_kernel_module_launch_spin_us\": %.2f, "
+         "\"extract_host_us\": %.2f, "
          "\"rms\": %.9g, \"centroid\": %.9g}\n",
          n, calls, median(ta), median(tl), median(tb), median(te), median(tf), median(tc), median(td), median(tg), median(th),
-         median(th2), median(ti), hout[0], hout[16]);
+         median(th2), median(th3), median(ti), hout[0], hout[16]);
   mgx_plan_destroy(p);
   return 0;
 }
