@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -917,6 +918,12 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
     e = hipStreamCreateWithFlags(&p->s_comp, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
   }
+  // (a one-frame call may return before its launch has ended (the output words below): nothing may free
+  // or reuse the pinned buffers under it)
+  if (p->h_in_bytes < in_bytes || p->h_out_bytes < out_bytes) {
+    e = hipStreamSynchronize(p->s_comp);
+    if (e != hipSuccess) return hip_fail(e, "small host batch (previous launch)");
+  }
   if (p->h_in_bytes < in_bytes) {
     if (p->h_in) (void)hipHostFree(p->h_in);
     p->h_in = nullptr;
@@ -992,18 +999,58 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
   }
   uint32_t* const ddone = p->d_done_map;
   p->done_seq = p->done_seq + 1 ? p->done_seq + 1 : 1;  // never 0, the word's initial value
+  // One frame without spectrum outputs (at most 13 + 24 + 32 words): the host waits on the output words
+  // themselves -- each preset to an all-ones NaN and polled until the kernel's store has landed -- and the
+  // launch releases no completion word, which spares the system-scope release (a wait for the outputs'
+  // write acknowledgements) and the word's own trip back. Stores of 4 and 8 aligned bytes arrive whole. An
+  // output that is itself that NaN (a NaN input can carry any payload) only ends the spin at its limit.
+  const bool word_wait = nframes == 1 && !o->amplitude_spectrum && !o->power_spectrum && !o->complex_real && !o->complex_imag;
+  constexpr uint64_t kSent = ~(uint64_t)0;
+  if (word_wait) {
+    for (int k = 0; k < MGX_NUM_SCALARS; ++k)
+      if (o->scalars[k]) memset(h.scalars[k], 0xFF, ss);
+    if (o->loudness_specific) memset(h.loudness_specific, 0xFF, nb * 4);
+    if (o->mfcc) memset(h.mfcc, 0xFF, nc * 4);
+    std::atomic_thread_fence(std::memory_order_release);
+  }
   // (one frame: also handed over in the kernel arguments, read there by the kernels that take it)
-  rc = extract_device_impl(p, static_cast<const float*>(din), nframes, &d, p->s_comp, ddone, nframes == 1 ? p->h_in : nullptr);
+  rc = extract_device_impl(p, static_cast<const float*>(din), nframes, &d, p->s_comp, word_wait ? nullptr : ddone,
+                           nframes == 1 ? p->h_in : nullptr);
   if (rc) {
     (void)hipStreamSynchronize(p->s_comp);
     return rc;
+  }
+  if (word_wait) {
+    const auto t0 = std::chrono::steady_clock::now();
+    bool late = false;
+    unsigned spins = 0;
+    auto wait_word = [&](const void* w, size_t bytes) {
+      for (;; ++spins) {
+        const uint64_t v = bytes == 8 ? __atomic_load_n(static_cast<const uint64_t*>(w), __ATOMIC_ACQUIRE)
+                                      : (uint64_t)__atomic_load_n(static_cast<const uint32_t*>(w), __ATOMIC_ACQUIRE);
+        if (v != (bytes == 8 ? kSent : (uint64_t)0xFFFFFFFFu)) return;
+        __builtin_ia32_pause();
+        if (late || ((spins & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSmallSpinUs))) {
+          late = true;
+          return;
+        }
+      }
+    };
+    for (int k = 0; k < MGX_NUM_SCALARS; ++k)
+      if (o->scalars[k]) wait_word(h.scalars[k], ss);
+    for (size_t i = 0; o->loudness_specific && i < nb; ++i) wait_word(h.loudness_specific + i, 4);
+    for (size_t i = 0; o->mfcc && i < nc; ++i) wait_word(h.mfcc + i, 4);
+    if (late) {  // a busy device, a failed launch, or an output equal to the preset: the stream decides
+      e = hipStreamSynchronize(p->s_comp);
+      if (e != hipSuccess) return hip_fail(e, "small host batch");
+    }
   }
   // The last wave of the launch releases done_seq to the host word after every output store is
   // visible (kernels.hip done_signal): polling it returns ~9 us sooner than waiting for the
   // stream (tools/ubench/small_latency.hip). Past 20 ms (a busy device) the wait blocks on the
   // stream instead, which also reports a failed launch. The spin pauses the core between reads
   // (a contended device leaves N-API worker threads waiting here) and gives up after kSmallSpinUs.
-  {
+  if (!word_wait) {
     const auto t0 = std::chrono::steady_clock::now();
     bool seen = false;
     for (unsigned spins = 0;; ++spins) {

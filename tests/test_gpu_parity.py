@@ -338,6 +338,24 @@ def test_one_frame_calls_with_the_frame_in_the_kernel_arguments(capi, n):
     p.close()
 
 
+def test_one_frame_call_whose_outputs_equal_the_wait_preset(capi):
+    """A one-frame host call without spectra waits on its output words, each preset to all ones (plan.cpp
+    extract_host_small). A frame of all-ones NaN samples can produce outputs with exactly that bit pattern
+    (the NaN payload propagates): the call must still end, through its spin limit and the stream, with the
+    device path's bits -- with float32 and float64 scalars."""
+    import torch
+    for f64 in (False, True):
+        p = capi.Plan(buffer_size=512, scalar_f64=f64)
+        x = np.full((1, 512), 0xFFFFFFFF, np.uint32).view(np.float32)
+        for feats in (["rms", "energy", "spectralCentroid"], capi.ALL_FEATURES):
+            a = p.extract(x, feats)
+            d = p.extract_torch(torch.from_numpy(x.copy()).cuda(), feats)
+            torch.cuda.synchronize()
+            for k in a:
+                assert np.array_equal(a[k].view(np.uint8), d[k].cpu().numpy().view(np.uint8)), (f64, k)
+        p.close()
+
+
 def test_small_and_staged_calls_alternate_on_one_plan(capi):
     """One plan serving small host batches (its own compute stream, created by the small path) and
     staged ones (which create the copy stream beside it) in turn, then destroyed: the staged path must
