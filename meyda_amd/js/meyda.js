@@ -290,7 +290,9 @@ class Meyda {
     if (!this._frame) this._frame = {};
     const need = names.filter((n) => !(n in this._frame));
     if (!need.length) return;
-    const r = extractViews(this._layouts, this._plan(), this._signal(), need, this.bufferSize, this.options.numMfccCoeffs);
+    // (into the layout's scratch buffer: frameValue copies every value out before anything else runs)
+    const r = extractViews(this._layouts, this._plan(), this._signal(), need, this.bufferSize, this.options.numMfccCoeffs,
+      true);
     for (const n of need) this._frame[n] = frameValue(n, r, 0, this.bufferSize, this.options.numMfccCoeffs);
   }
 
@@ -377,12 +379,12 @@ FIELDS.forEach((k, i) => { FIELD_BITS[k] = 2 ** i; });
 FIELD_BITS.loudness = FIELD_BITS['loudness.specific'] + FIELD_BITS['loudness.total'];
 FIELD_BITS.complexSpectrum = FIELD_BITS['complexSpectrum.real'] + FIELD_BITS['complexSpectrum.imag'];
 
-// Extraction of F frames into one fresh ArrayBuffer (addon.extractInto), its layout worked out once per
+// Extraction of F frames into one ArrayBuffer (addon.extractInto), its layout worked out once per
 // (output fields, F) and kept in the instance's `cache`: a result object of typed-array views with
 // extract()'s keys and shapes (scalars as Float64Array: the facade's plans use scalarF64). One
 // allocation and a few N-API calls per launch instead of an ArrayBuffer, a reference and a typed array
 // per output (the real-time paths).
-function extractViews(cache, plan, frames, names, N, nc) {
+function extractViews(cache, plan, frames, names, N, nc, scratch) {
   const F = frames.length / N;
   let bits = 0;
   for (let j = 0; j < names.length; j++) bits += FIELD_BITS[names[j]] || 0;  // (names are distinct)
@@ -404,11 +406,18 @@ function extractViews(cache, plan, frames, names, N, nc) {
     if (cache.size > 256) cache.clear();
     cache.set(key, lay);
   }
+  // scratch: the layout's own buffer and views, reused call after call (get(): the values are copied out at
+  // once); otherwise a fresh buffer whose views the caller may keep (the batched callbacks)
+  if (scratch && lay.scratch) {
+    addon.extractInto(plan, frames, lay.offsets, lay.scratch.ab);
+    return lay.scratch.r;
+  }
   const ab = new ArrayBuffer(lay.bytes);
   addon.extractInto(plan, frames, lay.offsets, ab);
   const r = {};
   const v = lay.views;
   for (let j = 0; j < v.length; j++) r[v[j][0]] = new v[j][1](ab, v[j][2], v[j][3]);
+  if (scratch) lay.scratch = { ab, r };
   return r;
 }
 
