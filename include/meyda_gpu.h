@@ -170,8 +170,13 @@ int mgx_plan_get_desc(const mgx_plan* plan, mgx_plan_desc* out_desc);
 int mgx_extract_device(mgx_plan* plan, const float* frames, uint64_t num_frames,
                        const mgx_outputs* outputs, void* stream);
 
-/* Host batch: frames and outputs in host memory; stages through plan-owned
- * device buffers in chunks and returns when the outputs are written. */
+/* Host batch: frames and outputs in host memory; returns when the outputs are
+ * written. Up to 512 frames run one launch over plan-owned pinned host memory
+ * (a single frame of N <= 512 samples inside the kernel arguments); larger
+ * batches stage through plan-owned device buffers in chunks. A one-frame call
+ * without spectrum outputs may return while the tail of its launch still runs
+ * on the plan's stream: later calls on the plan are ordered after it, and
+ * mgx_plan_destroy waits for it. */
 int mgx_extract_host(mgx_plan* plan, const float* frames, uint64_t num_frames,
                      const mgx_outputs* outputs);
 
