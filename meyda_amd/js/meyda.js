@@ -269,8 +269,13 @@ class Meyda {
   get(feature) {
     if (typeof feature === 'object') {
       const names = Array.prototype.slice.call(feature); // null throws, as feature.length does
+      const gpu = [];
+      for (let x = 0; x < names.length; x++) {
+        const n = names[x];
+        if (GPU_FEATURES.has(n) && !this.featureExtractors[n]) gpu.push(n);
+      }
       try {  // one launch for all built-in features; a failure resurfaces per feature below
-        this._compute(names.filter((n) => GPU_FEATURES.has(n) && !this.featureExtractors[n]));
+        this._compute(gpu);
       } catch (e) { /* logged per feature, as the reference does */ }
       const results = {};
       for (let x = 0; x < names.length; x++) {
@@ -293,8 +298,9 @@ class Meyda {
 
   // Compute the missing GPU features of the current buffer in one launch.
   _compute(names) {
-    if (!this._frame) this._frame = {};
-    const need = names.filter((n) => !(n in this._frame));
+    const fr = this._frame || (this._frame = {});
+    const need = [];
+    for (let x = 0; x < names.length; x++) if (!(names[x] in fr)) need.push(names[x]);
     if (!need.length) return;
     // (into the layout's scratch buffer: frameValue copies every value out before anything else runs)
     const r = extractViews(this._layouts, this._plan(), this._signal(), need, this.bufferSize, this.options.numMfccCoeffs,
@@ -305,6 +311,8 @@ class Meyda {
   _value(name) {
     const plugin = this.featureExtractors[name];
     if (plugin) return this._runPlugin(plugin);
+    const fr = this._frame;
+    if (fr && name in fr) return fr[name];  // this buffer's launch computed it
     if (name === 'buffer') return this._signal();
     if (!GPU_FEATURES.has(name)) {
       throw new TypeError("Cannot read property 'process' of undefined (feature '" + name + "')");
