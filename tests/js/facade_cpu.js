@@ -7,6 +7,7 @@
 const assert = require('assert');
 const path = require('path');
 const golden = require('./golden');
+const kernargPreset = process.env.HIP_FORCE_DEV_KERNARG;
 const Meyda = require(path.join(__dirname, '..', '..', 'meyda_amd', 'js', 'meyda.js'));
 
 const ctx = { sampleRate: 44100 };
@@ -102,6 +103,11 @@ check('bufferSize 1 and 2 construct (isPowerOfTwo accepts them; tables only)', (
   }
   const t = Meyda.addon.hostTables({ bufferSize: 1 });
   assert.strictEqual(t.barkLimits[24], -1);  // loudness.js:44: normalisedSpectrum.length - 1
+});
+
+check('the facade keeps kernel arguments in host memory unless the environment chose', () => {
+  // (set before the addon loaded the HIP runtime; a value the environment set is left as it was)
+  assert.strictEqual(process.env.HIP_FORCE_DEV_KERNARG, kernargPreset === undefined ? '0' : kernargPreset);
 });
 
 console.log('facade_cpu: ' + n + ' checks passed');

@@ -22,7 +22,7 @@ def run_node(script):
 
 def test_facade_host_side():
     out = run_node("facade_cpu.js")
-    assert "facade_cpu: 8 checks passed" in out
+    assert "facade_cpu: 9 checks passed" in out
 
 
 def test_facade_batched_delivery_host_side():
