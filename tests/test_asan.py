@@ -44,4 +44,4 @@ def test_js_facade_through_sanitized_addon():
     r = subprocess.run(["node", "--expose-gc", os.path.join(ROOT, "tests", "js", "facade_cpu.js")],
                        capture_output=True, text=True, env=e, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert "facade_cpu: 8 checks passed" in r.stdout
+    assert "facade_cpu: 9 checks passed" in r.stdout
