@@ -172,7 +172,7 @@ int mgx_extract_device(mgx_plan* plan, const float* frames, uint64_t num_frames,
 
 /* Host batch: frames and outputs in host memory; returns when the outputs are
  * written. Up to 512 frames run one launch over plan-owned pinned host memory
- * (a single frame of N <= 512 samples inside the kernel arguments); larger
+ * (a single frame of N <= 1024 samples inside the kernel arguments); larger
  * batches stage through plan-owned device buffers in chunks. A one-frame call
  * without spectrum outputs may return while the tail of its launch still runs
  * on the plan's stream: later calls on the plan are ordered after it, and

@@ -817,8 +817,7 @@ __device__ __forceinline__ KArgs* args_ptr() {
 
 // KernelArgsInline::frame of a one-frame launch that carries its frame in the kernel arguments (INL)
 __device__ __forceinline__ const float* inline_frame_ptr() {
-  const auto q = (const __attribute__((address_space(4))) KernelArgsInline*)args_ptr();
-  return (const float*)q->frame;
+  return (const float*)((const __attribute__((address_space(4))) unsigned char*)args_ptr() + kInlineFrameOff);
 }
 
 // Pointers read through args_ptr() are generic; re-type them as global (address space 1)
@@ -1906,7 +1905,7 @@ __device__ unsigned long long g_wave_times[65536 * 4];
 
 template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN, bool INL = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(
-    std::conditional_t<INL, KernelArgsInline, KernelArgs> a) {
+    std::conditional_t<INL, KernelArgsInline<N>, KernelArgs> a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   using LY = Lds<N>;
@@ -2368,8 +2367,8 @@ template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false,
 hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream, const float* inl = nullptr) {
   const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
   if constexpr (N <= kInlineMaxN && FAITH && !LITERAL && !CHAIN) {
-    if (inl) {  // the one frame in the kernel arguments (KernelArgsInline)
-      KernelArgsInline x;
+    if (inl) {  // the one frame in the kernel arguments (KernelArgsInline<N>)
+      KernelArgsInline<N> x;
       x.a = a;
       memcpy(x.frame, inl, N * sizeof(float));
       hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN, true>), dim3(grid), dim3(kThreads), lds,
@@ -2513,7 +2512,7 @@ hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, i
   switch (n) {
     case 256: return launch_prec<256>(precision, mode, a, grid, stream, inline_frame);
     case 512: return launch_prec<512>(precision, mode, a, grid, stream, inline_frame);
-    case 1024: return launch_prec<1024>(precision, mode, a, grid, stream, nullptr);
+    case 1024: return launch_prec<1024>(precision, mode, a, grid, stream, inline_frame);
     case 2048: return launch_prec<2048>(precision, mode, a, grid, stream, nullptr);
     default: return hipErrorInvalidValue;
   }

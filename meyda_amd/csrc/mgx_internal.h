@@ -1,6 +1,7 @@
 // Internal definitions shared by the host plan code and the HIP kernels.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/meyda_gpu.h"
@@ -96,11 +97,16 @@ struct KernelArgs {
 // its frame in the kernel arguments, after the KernelArgs: the kernel's first loads read it from the
 // kernarg segment, whose address the wave holds from its first instruction, instead of waiting for the
 // arguments before it can issue the frame's read of pinned host memory over PCIe.
-constexpr int kInlineMaxN = 512;
+constexpr int kInlineMaxN = 1024;  // (4,528 bytes of arguments at N = 1024: tools/ubench/kernarg_size.hip runs 4.8 KB)
+template <int N>
 struct KernelArgsInline {
   KernelArgs a;
-  alignas(16) float frame[kInlineMaxN];
+  alignas(16) float frame[N];
 };
+// (the frame's offset in the kernel arguments, the same for every N)
+constexpr size_t kInlineFrameOff = (sizeof(KernelArgs) + 15) / 16 * 16;
+static_assert(offsetof(KernelArgsInline<256>, frame) == kInlineFrameOff && offsetof(KernelArgsInline<2048>, frame) == kInlineFrameOff,
+              "inline frame offset");
 
 // Last-error reporting (plan.cpp): set mgx_last_error() and return `code`.
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));

@@ -313,9 +313,9 @@ def test_small_host_batches_equal_staged_path(capi, n):
             assert np.array_equal(a2[k].view(np.uint8), b2[k].view(np.uint8)), (F, k, "second call")
 
 
-@pytest.mark.parametrize("n", [256, 512])
+@pytest.mark.parametrize("n", [256, 512, 1024])
 def test_one_frame_calls_with_the_frame_in_the_kernel_arguments(capi, n):
-    """A one-frame host call at N <= 512 passes its frame inside the kernel arguments (KernelArgsInline;
+    """A one-frame host call at N <= 1024 passes its frame inside the kernel arguments (KernelArgsInline;
     kernels.hip extract_kernel<..., INL>): each kernel kind that takes it -- every feature, a subset (SUB),
     a light subset (LIGHT: mfcc or a spectrum alone), every spectral feature without the time-domain ones
     (NOTIME) -- must give the device path's bits, for ordinary and for non-finite frames, call after call."""
