@@ -7,7 +7,8 @@
 //   D  the kernel's own duration between two events, G  the same on device-resident frames and outputs,
 //   H  a kernel that only releases a sequence number to a mapped host word, the host spinning on it (the
 //      protocol's floor), H2 the same with 2,480 bytes of kernel arguments, H3 the same through
-//      hipModuleLaunchKernel with pre-packed arguments, I  mgx_extract_host itself.
+//      hipModuleLaunchKernel with pre-packed arguments, I  mgx_extract_host itself, J  one hipSetDevice call
+//      (0.07 us: the small path's two per call cost nothing measurable).
 // Build: hipcc --offload-arch=gfx950 -O2 -I include -o tools/ubench/small_latency tools/ubench/small_latency.hip \
 //          -L meyda_amd -lmeyda_gpu -Wl,-rpath,$PWD/meyda_amd
 // usage: small_latency [N] [calls]
@@ -216,6 +217,11 @@ int main(int argc, char** argv) {
       th3.push_back(t18 - t17);
     }
   }
+  // J: the cost of one hipSetDevice call (the small host path makes two per call)
+  double tj0 = now_us();
+  for (int i = 0; i < 20000; ++i) CK(hipSetDevice(0));
+  const double set_device_us = (now_us() - tj0) / 20000;
+  printf("{\"set_device_us\": %.3f}\n", set_device_us);
   printf("{\"n\": %d, \"calls\": %d, \"launch_sync_us\": %.2f, \"launch_call_us\": %.2f, \"launch_spin_us\": %.2f, "
          "\"launch_stream_query_us\": %.2f, \"launch_event_query_us\": %.2f, "
          "\"empty_kernel_sync_us\": %.2f, \"kernel_event_us\": %.2f, \"kernel_event_device_io_us\": %.2f, "
