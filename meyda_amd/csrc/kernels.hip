@@ -1984,7 +1984,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // SIMD's arbiter favours the oldest wave, so with equal shares rank 0 finished at 64 % of
   // the launch and the SIMDs ran 3, 2, then 1 wave for the rest (tools/wave_times.py).
   // Rank r takes a share of its own instead (22 / 18 / 14 / 10 of 64 at N = 1024).
-  const uint64_t ng = (nb + 3) / 4;
+  // (the tail pool: the static shares cover the first ng - pool_groups groups, kPool kernels only)
+  constexpr bool kPool = G::PF == 0 && !CHAIN && !INL;
+  const uint64_t ng_all = (nb + 3) / 4;
+  const uint64_t pool_groups = kPool ? (uint64_t)args_ptr()->pool_groups : 0;
+  const uint64_t ng = ng_all - (pool_groups < ng_all ? pool_groups : ng_all);
   uint64_t g0, g1;
   const uint64_t nr = (uint64_t)nr32;
   // (unequal shares need many groups per workgroup: with a few each, their rounding unbalances
@@ -2101,7 +2105,36 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
 
   MGX_STAMP(2);
   int it = 0;  // the wave's batch count (CHAIN with paired batches: the pair's second when odd)
-  for (uint64_t b = b0; b < bend; b += wstride, ++it) {
+  // The static batches (stride wstride from b0), then, with a tail pool, batches taken by ticket; a stolen
+  // batch does not count in `it` (the scalar windows and pairs follow the static batches only).
+  bool stolen = false;
+  for (uint64_t b = b0;;) {
+    if (!stolen && b >= bend) {
+      if (!kPool || pool_groups == 0) break;
+      if (kScalDefer && args_ptr()->scal_defer && (it & (kScalBatches - 1)) != 0) {
+        // the wave's last window of static batches, before its batches from the pool
+        KArgs* q = args_ptr();
+        const int nbat = it & (kScalBatches - 1), l2 = opaque(lane);
+        scalar_pass<N, SUB>(q, uniform_ptr(gbl(q->scal_rows) + ((uint64_t)blockIdx.x * 4 + wave) * (uint64_t)kScalWords),
+                            reinterpret_cast<void* const*>(smem + LY::kc_off), (b0 + (uint64_t)(it - nbat) * wstride) * FPW,
+                            wstride * FPW, nbat, l2);
+        it = (it + kScalBatches) & ~(kScalBatches - 1);  // (the window is flushed: nothing left for the end)
+      }
+      stolen = true;
+    }
+    if (stolen) {
+      // one ticket per batch (lane 0's vector atomic, the value to every lane); every wave ends on the first
+      // ticket past the pool, so a launch consumes exactly pool batches + waves tickets
+      KArgs* q = args_ptr();
+      uint64_t t = 0;
+      if (lane == 0) t = __hip_atomic_fetch_add(gbl(q->pool_ctr), (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)t) |
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(t >> 32)) << 32);
+      t -= q->pool_base;
+      const uint64_t first = ng * 4;
+      if (t >= nb - first) break;
+      b = first + t;
+    }
     const uint64_t f0 = b * FPW;
     // ------------------------------------------------------------- phase 1
     for (int j = 0; j < FPW; ++j) {
@@ -2211,7 +2244,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         if (CHAIN && q->chain_pair) mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 32, f0 - wstride * FPW);  // the pair's first batch
       }
       MGX_MARK(dct_done);
-      const bool defer = kScalDefer && q->scal_defer;
+      const bool defer = kScalDefer && q->scal_defer && !stolen;
       if (defer) {
         // the batch's scalar inputs into the wave's window (10 words per frame, lanes 0..39: frame
         // l2 / 10, word l2 % 10), the scalars of the window once it is full (scalar_pass)
@@ -2249,12 +2282,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     // all four reach the same barriers. N = 512 and 2048 lost 1.6 % and 2.3 % and keep none.
     if constexpr (G::GROUP_SYNC > 0) {
       const uint64_t g = (b - wave) / 4;
-      if (g * 4 + 3 < nb && g % G::GROUP_SYNC == G::GROUP_SYNC - 1) __builtin_amdgcn_s_barrier();
+      if (!stolen && g * 4 + 3 < nb && g % G::GROUP_SYNC == G::GROUP_SYNC - 1) __builtin_amdgcn_s_barrier();
     }
     // A full scalar window: its pass right after the group barrier (a window ends on an odd group,
     // where the barrier is), so the workgroup's four waves write their 16-byte pieces of each
     // scalar output line together and the L2 merges them, as the per-batch form's writes.
-    if (kScalDefer && (it & (kScalBatches - 1)) == kScalBatches - 1) {
+    if (kScalDefer && !stolen && (it & (kScalBatches - 1)) == kScalBatches - 1) {
       KArgs* q = args_ptr();
       if (q->scal_defer) {
         prio_hi<4>();
@@ -2263,6 +2296,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
                             (b - (uint64_t)(kScalBatches - 1) * wstride) * FPW, wstride * FPW, kScalBatches, opaque(lane));
         prio_lo<4>();
       }
+    }
+    if (!stolen) {
+      b += wstride;
+      ++it;
     }
   }
   if (kScalDefer && args_ptr()->scal_defer && (it & (kScalBatches - 1)) != 0) {

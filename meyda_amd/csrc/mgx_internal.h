@@ -91,6 +91,13 @@ struct KernelArgs {
   int chain_pair;        // the chains of two consecutive batches of a wave run together (8 frames, nfilt <= 31)
   float* chain_rows;     // the chains' power rows: 2 FPW x N/2 floats per wave of the grid (kernels.hip mel_chains)
   uint64_t* scal_rows;   // the scalar window: kScalWords 8-byte words per wave of the grid (kernels.hip scalar_pass)
+  // The tail pool (kernels without a frame prefetch, i.e. N = 2048; 0 groups = off): the last pool_groups
+  // groups of 4 batches are left out of the static shares and taken one batch per ticket by the waves
+  // that finish their share first. pool_ctr is the launching stream's ticket counter (monotonic: a launch
+  // consumes its pool's batches plus one failing ticket per wave, and the next starts at pool_base).
+  uint64_t* pool_ctr;
+  uint64_t pool_base;
+  uint32_t pool_groups;
 };
 
 // A one-frame launch at N <= kInlineMaxN (the real-time path: extract_host_small with one frame) carries

@@ -466,6 +466,8 @@ struct mgx_plan {
     uint64_t* scal;
     float* rows;  // null until a reference-order MFCC launch on the stream
     hipEvent_t done;
+    uint64_t* pool_ctr = nullptr;  // the tail pool's ticket counter (KernelArgs::pool_ctr), and its next base
+    uint64_t pool_base = 0;
   };
   std::vector<ChainRing> chain_rings;
   // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
@@ -479,6 +481,7 @@ struct mgx_plan {
   hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr}, ev_back[2] = {nullptr, nullptr};
   // small host batches (kSmallBatchFrames): pinned, device-mapped, coherent host buffers
   uint64_t small_max = kSmallBatchFrames;
+  int pool_pct = 0;  // the N = 2048 tail pool's share of the groups, percent (MGX_POOL_PCT; 0: off)
   // the small path's completion word (KernelArgs::done_flag): a mapped host word, the device
   // counter of finished waves and the launch sequence number
   uint32_t* h_done = nullptr;
@@ -633,6 +636,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
     else if (atoi(gc) > 0) p->grid_cap = atoi(gc);
   }
   if (const char* sb = getenv("MGX_SMALL_BATCH_FRAMES")) p->small_max = (uint64_t)std::max(0, atoi(sb));
+  if (const char* pp = getenv("MGX_POOL_PCT")) p->pool_pct = std::min(50, std::max(0, atoi(pp)));
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
@@ -708,6 +712,7 @@ int mgx_plan_destroy(mgx_plan* p) {
     (void)hipEventDestroy(r.done);
     if (r.scal) (void)hipFree(r.scal);
     if (r.rows) (void)hipFree(r.rows);
+    if (r.pool_ctr) (void)hipFree(r.pool_ctr);
   }
   for (int i = 0; i < 2; ++i) {
     if (p->s_frames[i]) (void)hipFree(p->s_frames[i]);
@@ -803,7 +808,7 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
     hipEvent_t done = nullptr;
     e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
     if (e != hipSuccess) return hip_fail(e, "hipEventCreate(stream scratch)");
-    p->chain_rings.push_back({stream, nullptr, nullptr, done});
+    p->chain_rings.push_back({stream, nullptr, nullptr, done, nullptr, 0});
     ring = &p->chain_rings.back();
   }
   if (a.scal_defer) {
@@ -827,6 +832,25 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
     }
     a.chain_rows = ring->rows;
   }
+  // The tail pool at N = 2048 (the kernels without a frame prefetch; not the reference-order ones): the
+  // last MGX_POOL_PCT percent of the groups taken by ticket (kernels.hip; default 0: off).
+  uint64_t pool_batches = 0;
+  if (p->n == 2048 && !(a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) && p->pool_pct > 0) {
+    // (nb here counts groups of 16 frames, the kernel's groups; the pool's tickets are batches of 4 frames)
+    const uint64_t ng_all = nb, pg = ng_all * (uint64_t)p->pool_pct / 100, batches = (nframes + 3) / 4;
+    if (pg > 0 && pg < ng_all) {
+      if (!ring->pool_ctr) {
+        e = hipMalloc(reinterpret_cast<void**>(&ring->pool_ctr), sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMemsetAsync(ring->pool_ctr, 0, sizeof(uint64_t), (hipStream_t)stream);
+        if (e != hipSuccess) return hip_fail(e, "tail pool counter");
+        ring->pool_base = 0;
+      }
+      a.pool_ctr = ring->pool_ctr;
+      a.pool_base = ring->pool_base;
+      a.pool_groups = (uint32_t)pg;
+      pool_batches = batches - (ng_all - pg) * 4;
+    }
+  }
   // (a launch on the plan's own compute stream records no event: destroy synchronises that
   // stream, and the small host path saves the record's ~1 us per call)
   // (a NULL caller stream is never the plan's: s_comp may not exist yet, and then both are NULL)
@@ -839,6 +863,8 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
   }
   e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream, inline_frame);
   if (e != hipSuccess) return hip_fail(e, "extract kernel launch");
+  // (every wave ends on one ticket past the pool: the launch consumes its pool's batches plus one per wave)
+  if (a.pool_groups) ring->pool_base += pool_batches + (uint64_t)grid * 4;
   if (ring_done) {
     e = hipEventRecord(ring_done, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord(mel chain rows)");

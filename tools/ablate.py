@@ -21,11 +21,11 @@ PATCHES = {
     "no_dct": [("        mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 0, f0);",
                 "        if (opaque(0)) mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 0, f0);")],
     # (the window copies in phase 2 and the scalar passes, kScalDefer)
-    "no_scalars": [("      const bool defer = kScalDefer && q->scal_defer;", "      const bool defer = opaque(0);"),
+    "no_scalars": [("      const bool defer = kScalDefer && q->scal_defer && !stolen;", "      const bool defer = opaque(0);"),
                    ("for (int i = l2; !defer && i <", "for (int i = l2; opaque(0) && i <"),
                    ("      if (q->scal_defer) {\n        prio_hi<4>();", "      if (opaque(0)) {\n        prio_hi<4>();"),
-                   ("  if (kScalDefer && args_ptr()->scal_defer && (it & (kScalBatches - 1)) != 0) {",
-                    "  if (opaque(0) && (it & (kScalBatches - 1)) != 0) {")],
+                   ("  if (kScalDefer && args_ptr()->scal_defer && (it & (kScalBatches - 1)) != 0) {\n    // the wave's last window",
+                    "  if (opaque(0) && (it & (kScalBatches - 1)) != 0) {\n    // the wave's last window")],
     # the frame samples from the address instead of HBM (is the frame load's latency exposed?)
     "no_frame_load": [("  if constexpr (NT) return __builtin_nontemporal_load(p);\n  return *p;",
                        "  const uint32_t a = (uint32_t)(uintptr_t)p; return (float)((a >> 2) & 1023) * 0x1p-10f - 0.5f;")],
