@@ -481,7 +481,7 @@ struct mgx_plan {
   hipEvent_t ev_loaded[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr}, ev_back[2] = {nullptr, nullptr};
   // small host batches (kSmallBatchFrames): pinned, device-mapped, coherent host buffers
   uint64_t small_max = kSmallBatchFrames;
-  int pool_pct = 0;  // the N = 2048 tail pool's share of the groups, percent (MGX_POOL_PCT; 0: off)
+  int pool_pct = 15;  // the N = 2048 tail pool's share of the groups, percent (MGX_POOL_PCT overrides; 0: off)
   // the small path's completion word (KernelArgs::done_flag): a mapped host word, the device
   // counter of finished waves and the launch sequence number
   uint32_t* h_done = nullptr;
@@ -833,7 +833,8 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
     a.chain_rows = ring->rows;
   }
   // The tail pool at N = 2048 (the kernels without a frame prefetch; not the reference-order ones): the
-  // last MGX_POOL_PCT percent of the groups taken by ticket (kernels.hip; default 0: off).
+  // last pool_pct percent of the groups taken by ticket (kernels.hip; 15 %: -2.7 % per launch against the static
+  // shares alone, outputs identical, profiles/r05_tail_pool.txt).
   uint64_t pool_batches = 0;
   if (p->n == 2048 && !(a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) && p->pool_pct > 0) {
     // (nb here counts groups of 16 frames, the kernel's groups; the pool's tickets are batches of 4 frames)
