@@ -239,12 +239,17 @@ def latency_js():
         return {"status": "skipped (node not found)"}
     if not os.path.exists(addon):
         return {"status": "skipped (meyda_amd/addon/meyda_napi.node not built)"}
+    # the application-side setting INTEGRATION.md recommends for the real-time path (the facade itself
+    # leaves the environment alone): kernel arguments in host memory
+    env = dict(os.environ)
+    env.setdefault("HIP_FORCE_DEV_KERNARG", "0")
     r = subprocess.run(["node", os.path.join(ROOT, "tools", "latency.js")], capture_output=True, text=True,
-                       timeout=240)
+                       timeout=240, env=env)
     if r.returncode != 0:
         return {"status": "failed (rc %d): %s" % (r.returncode, r.stderr.strip()[-400:])}
     out = json.loads(r.stdout.strip().splitlines()[-1])
     out["status"] = "ok"
+    out["env"] = {"HIP_FORCE_DEV_KERNARG": env["HIP_FORCE_DEV_KERNARG"]}
     return out
 
 
@@ -629,6 +634,29 @@ def c5_field(gpus, F5, el, km, stats, steps, gather_on, chunks=0):
     return c5
 
 
+def c5_finish(c5, gpus):
+    """C5's `value` as BASELINE.json configs[4] defines it ("frames sharded across GPUs with RCCL gather"):
+    at N > 1 the gather-inclusive rate of the same steps (every rank's records to rank 0 inside each timed
+    step), None when the gather did not complete; at N = 1 the one shard (nothing to gather). The shards'
+    rate without the gather stays beside it as `shards_value`. Idempotent (a deadline may print the line
+    before the gather phase ends)."""
+    shards = c5.setdefault("shards_value", c5["value"])
+    g = c5.get("gather") or {}
+    if gpus == 1:
+        c5["value"] = shards
+        c5["value_source"] = "one GPU: its shard alone (nothing to gather)"
+    elif g.get("status") == "ok":
+        c5["value"] = g["value"]
+        g["vs_shards"] = g["value"] / shards
+        c5["value_source"] = ("gather-inclusive: every rank's feature records gathered to rank 0 over RCCL inside each "
+                              "timed step (gather.*); shards_value: the shards alone, no data-path collective")
+    else:
+        c5["value"] = None
+        c5["value_source"] = ("no gather-inclusive rate (gather: %s); shards_value: the shards alone"
+                              % g.get("status", "not run"))
+    return c5
+
+
 def main():
     args = parse()
     from meyda_amd import dist as mdist
@@ -711,8 +739,6 @@ def main():
                 emit_line()
                 os._exit(code)
             wd.t.join()  # a failed peer waits for its deadline (rank 0 may be blocked on it)
-    if c5 is not None and "gather" in c5 and c5["gather"].get("status") == "ok":
-        c5["gather"]["vs_shards"] = c5["gather"]["value"] / c5["value"]
     emit_line()
     if dist:
         dist.barrier()
@@ -928,6 +954,8 @@ def build_line(args, gpus, mode, placement, F, n, value_s, el_s, km_s, stats_s, 
               "cpu_baseline"):
         if k in extras:
             line[k] = extras[k]
+    if line.get("c5"):
+        c5_finish(line["c5"], gpus)
     if "mfcc_exact" in line and line["mfcc_exact"].get("kernel_ms"):
         line["mfcc_exact"]["cost_vs_value_kernel"] = line["mfcc_exact"]["kernel_ms"] / kernel_ms - 1.0
     return line

@@ -162,11 +162,13 @@ int mgx_plan_get_desc(const mgx_plan* plan, mgx_plan_desc* out_desc);
 /* Device-resident batch: frames and every non-NULL output are device pointers.
  * Asynchronous on `stream` (hipStream_t or NULL). The launch uses per-stream device scratch,
  * one set per distinct stream the plan launches on: the scalar features' windows (5 KB per
- * resident wave, ~20 MB) and, for a plan with MGX_FLAG_MFCC_REFERENCE and an MFCC output, the
- * power-row ring of its mel chains (~2 KB x 8 per resident wave, tens of MB). A set is allocated
- * on the first call on its stream (hipMalloc, which may synchronise the device: make one
- * untimed call per stream first, outside any stream capture) and kept until mgx_plan_destroy,
- * which waits for the launches that used it. */
+ * resident wave, ~20 MB), for a plan with MGX_FLAG_MFCC_REFERENCE the power-row ring of its mel
+ * chains (~2 KB x 8 per resident wave, tens of MB), and at N = 2048 the tail pool's ticket
+ * counter (8 bytes). The whole set is allocated by the first call on its stream, whatever that
+ * call's size or outputs (hipMalloc, which may synchronise the device: make one untimed call per
+ * stream first, outside any stream capture), and kept until mgx_plan_destroy, which waits for
+ * the launches that used it. After that first call a launch keeps no host-side state between
+ * calls: it may be captured into a HIP graph and replayed any number of times. */
 int mgx_extract_device(mgx_plan* plan, const float* frames, uint64_t num_frames,
                        const mgx_outputs* outputs, void* stream);
 

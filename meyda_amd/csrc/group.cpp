@@ -337,21 +337,24 @@ int ipc_join(mgx_group* g, const char* id, uint32_t rank) {
     return fail(MGX_E_INVALID_ARGUMENT, "MGX_GROUP_TRANSPORT=ipc: the group id was not made by mgx_comm_unique_id in this mode");
   if (g->nranks > kIpcMaxRanks) return fail(MGX_E_UNSUPPORTED, "the IPC transport holds at most %u ranks", kIpcMaxRanks);
   IpcLink& L = g->ipc;
-  L.name = std::string("/") + (id + sizeof kIpcTag - 1);
+  // (L.name -- the name ipc_leave unlinks -- is set only once this rank has opened the mailbox: a name
+  // that already existed, or never appeared, belongs to someone else and is left alone)
+  const std::string name = std::string("/") + (id + sizeof kIpcTag - 1);
   const size_t bytes = sizeof(IpcMail);
   int fd = -1;
   const double tmo = ipc_timeout_s();
   if (rank == 0) {
-    fd = shm_open(L.name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
-    if (fd < 0) return fail(MGX_E_DEVICE, "shm_open(%s): %s", L.name.c_str(), strerror(errno));
+    fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0) return fail(MGX_E_DEVICE, "shm_open(%s): %s", name.c_str(), strerror(errno));
     if (ftruncate(fd, (off_t)bytes) != 0) {
       close(fd);
-      shm_unlink(L.name.c_str());
+      shm_unlink(name.c_str());
       return fail(MGX_E_DEVICE, "ftruncate(mailbox): %s", strerror(errno));
     }
-  } else if (!ipc_wait([&] { return (fd = shm_open(L.name.c_str(), O_RDWR, 0600)) >= 0; }, tmo)) {
-    return fail(MGX_E_DEVICE, "rank %u: the group mailbox %s never appeared", rank, L.name.c_str());
+  } else if (!ipc_wait([&] { return (fd = shm_open(name.c_str(), O_RDWR, 0600)) >= 0; }, tmo)) {
+    return fail(MGX_E_DEVICE, "rank %u: the group mailbox %s never appeared", rank, name.c_str());
   }
+  L.name = name;
   void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   if (p == MAP_FAILED) return fail(MGX_E_DEVICE, "mmap(mailbox): %s", strerror(errno));

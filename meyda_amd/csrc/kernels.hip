@@ -116,14 +116,12 @@ struct Geo {
   // before it: prefetching at the start of the frame made every frame wait for the next
   // one's HBM read at its window step (at N = 1024 loading each frame only when its wave
   // starts it was 2.7 % faster).
-// PF = 1 loads the next frame at the start of this one; PF = 2 issues it in the middle of
+  // PF = 1 loads the next frame at the start of this one; PF = 2 issues it in the middle of
   // this frame, after the last table loads this frame waits on (twiddles: the passes are
   // done; the mel records: issued just before), so no wait of this frame is held up by
-  // it; PF = 0 loads each frame when its wave starts it.
-#ifndef MGX_PF_2048
-#define MGX_PF_2048 0
-#endif
-  static constexpr int PF = N <= 256 ? 1 : N <= 1024 ? 2 : MGX_PF_2048;  // measured best per N
+  // it; PF = 0 loads each frame when its wave starts it (N = 2048: a mid-frame prefetch
+  // measured -0.3 %, noise, and costs the tail pool, which needs PF = 0).
+  static constexpr int PF = N <= 256 ? 1 : N <= 1024 ? 2 : 0;  // measured best per N
   // WIN_REG: the window held in registers for the whole launch (CH VGPRs) instead of loaded
   // per frame (N = 1024, where the LDS twiddles freed the registers: 1.1-1.5 % faster, 119
   // VGPRs; the frame prefetch at the frame's start instead, PF = 1, 0.9-1.1 %, and both
@@ -304,10 +302,6 @@ __device__ __forceinline__ void st_out(P p, float v) {
   __builtin_nontemporal_store(v, p);
 }
 
-// (A/B: -DMGX_NT_FRAMES=1 loads every kernel's frames non-temporally, as the CHAIN kernel's)
-#ifndef MGX_NT_FRAMES
-#define MGX_NT_FRAMES 0
-#endif
 template <bool NT = false>
 __device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))) float* p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -760,13 +754,10 @@ struct ScalIn {
 static_assert(sizeof(ScalIn) == 80, "10 words");
 static_assert(offsetof(FrameRec, band) == 56 && offsetof(FrameRec, zcr) == 504 && offsetof(FrameRec, sharp_sum) == 516,
               "the scalar inputs: FrameRec words 0..7 and 63..64");
-#ifndef MGX_SCAL_DEFER
-#define MGX_SCAL_DEFER 1
-#endif
 // Scalars once per window of kScalBatches batches, one lane per frame (scalar_pass), instead of
 // one lane per (feature, frame) in every batch's phase 2 -- for launches that compute a spectrum
 // (KernelArgs::scal_defer; plan.cpp says when)
-constexpr bool kScalDefer = MGX_SCAL_DEFER;
+constexpr bool kScalDefer = true;
 
 // Record fb (< 4) of the wave's batch and small per-lane offsets by 24-bit multiplies: the lane
 // indices come through opaque() (no range the compiler can see), and a 32-bit v_mul_lo_u32 /
@@ -1114,7 +1105,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   auto prefetch_next = [&]() {
     if constexpr (G::PF == 2) {
 #pragma unroll
-      for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN || MGX_NT_FRAMES>(next + (c * 64 + (unsigned)lane));
+      for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN>(next + (c * 64 + (unsigned)lane));
     }
   };
   // The window: held in registers for the launch at N = 1024 (Geo::WIN_REG); otherwise its
@@ -2051,7 +2042,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   auto load = [&](float (&xv)[CH], uint64_t b, int j) {
     const GF xin = frame_ptr(b, j);
 #pragma unroll
-    for (int c = 0; c < CH; ++c) xv[c] = ld_frame<CHAIN || MGX_NT_FRAMES>(xin + (c * 64 + (unsigned)lane));
+    for (int c = 0; c < CH; ++c) xv[c] = ld_frame<CHAIN>(xin + (c * 64 + (unsigned)lane));
   };
 
   // The workgroup's LDS tables, from the plan's image (lds_image_kernel) in one pass of 16-byte loads,
@@ -2076,7 +2067,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     const uint64_t f = b0 * FPW < nf ? b0 * FPW : nf - 1;
     const GF xin = (GF)uniform_ptr(gbl(frames_p) + f * (uint64_t)N);
 #pragma unroll
-    for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN || MGX_NT_FRAMES>(xin + (c * 64 + (unsigned)lane));
+    for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN>(xin + (c * 64 + (unsigned)lane));
   }
   // the output pointers, then the image's chunks
   if (threadIdx.x < MGX_NUM_SCALARS) reinterpret_cast<void**>(smem + LY::kc_off)[threadIdx.x] = kp;
@@ -2124,15 +2115,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     }
     if (stolen) {
       // one ticket per batch (lane 0's vector atomic, the value to every lane); every wave ends on the first
-      // ticket past the pool, so a launch consumes exactly pool batches + waves tickets
+      // ticket past the pool, so a launch hands out exactly pool batches + waves tickets, from 0. The wave that
+      // draws the last of them resets the counter: every other ticket of the launch was drawn before it (the
+      // counter's order), and no wave draws again, so the next launch on the stream -- or the next replay of
+      // a captured one -- starts from 0 with no state kept on the host.
       KArgs* q = args_ptr();
       uint64_t t = 0;
-      if (lane == 0) t = __hip_atomic_fetch_add(gbl(q->pool_ctr), (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t first = ng * 4, pool = nb - first, last = pool + (uint64_t)grid * 4 - 1;
+      if (lane == 0) {
+        t = __hip_atomic_fetch_add(gbl(q->pool_ctr), (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == last) __hip_atomic_store(gbl(q->pool_ctr), (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       t = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)t) |
           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(t >> 32)) << 32);
-      t -= q->pool_base;
-      const uint64_t first = ng * 4;
-      if (t >= nb - first) break;
+      if (t >= pool) break;
       b = first + t;
     }
     const uint64_t f0 = b * FPW;

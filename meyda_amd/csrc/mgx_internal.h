@@ -93,10 +93,10 @@ struct KernelArgs {
   uint64_t* scal_rows;   // the scalar window: kScalWords 8-byte words per wave of the grid (kernels.hip scalar_pass)
   // The tail pool (kernels without a frame prefetch, i.e. N = 2048; 0 groups = off): the last pool_groups
   // groups of 4 batches are left out of the static shares and taken one batch per ticket by the waves
-  // that finish their share first. pool_ctr is the launching stream's ticket counter (monotonic: a launch
-  // consumes its pool's batches plus one failing ticket per wave, and the next starts at pool_base).
+  // that finish their share first. pool_ctr is the launching stream's ticket counter: 0 when a launch starts,
+  // and reset to 0 on the device by the wave that draws the launch's last ticket (kernels.hip), so a launch
+  // captured into a graph replays with no host state.
   uint64_t* pool_ctr;
-  uint64_t pool_base;
   uint32_t pool_groups;
 };
 

@@ -466,8 +466,7 @@ struct mgx_plan {
     uint64_t* scal;
     float* rows;  // null until a reference-order MFCC launch on the stream
     hipEvent_t done;
-    uint64_t* pool_ctr = nullptr;  // the tail pool's ticket counter (KernelArgs::pool_ctr), and its next base
-    uint64_t pool_base = 0;
+    uint64_t* pool_ctr = nullptr;  // the tail pool's ticket counter (KernelArgs::pool_ctr; N = 2048 plans)
   };
   std::vector<ChainRing> chain_rings;
   // two device slots for mgx_extract_host (copy of chunk i+1 beside the extraction of chunk i)
@@ -745,6 +744,38 @@ int mgx_extract_device(mgx_plan* p, const float* frames, uint64_t nframes, const
 
 namespace {
 
+// A stream's scratch set (mgx_plan::ChainRing), the whole set at once: the scalar windows (kScalWords words
+// for each wave of the largest grid), the reference-order MFCC's power-row ring (2 FPW x N/2 floats per wave;
+// MGX_FLAG_MFCC_REFERENCE plans) and the tail pool's ticket counter (N = 2048 plans), zeroed in stream order
+// before the first launch. On failure nothing is kept and the next call on the stream tries again.
+int add_stream_scratch(mgx_plan* p, void* stream) {
+  mgx_plan::ChainRing r{};
+  r.stream = stream;
+  auto undo = [&r]() {
+    if (r.done) (void)hipEventDestroy(r.done);
+    if (r.scal) (void)hipFree(r.scal);
+    if (r.rows) (void)hipFree(r.rows);
+    if (r.pool_ctr) (void)hipFree(r.pool_ctr);
+  };
+  hipError_t e = hipEventCreateWithFlags(&r.done, hipEventDisableTiming);
+  if (e != hipSuccess) { r.done = nullptr; return hip_fail(e, "hipEventCreate(stream scratch)"); }
+  e = hipMalloc(reinterpret_cast<void**>(&r.scal), (size_t)p->grid_cap * 4 * mgx::kScalWords * sizeof(uint64_t));
+  if (e != hipSuccess) { r.scal = nullptr; undo(); return hip_fail(e, "hipMalloc(scalar windows)"); }
+  if (p->chain_groups > 0) {
+    const size_t fpw = (size_t)mgx::frames_per_batch(p->n) / 4;
+    e = hipMalloc(reinterpret_cast<void**>(&r.rows), (size_t)p->grid_cap * 4 * 2 * fpw * (size_t)p->L * sizeof(float));
+    if (e != hipSuccess) { r.rows = nullptr; undo(); return hip_fail(e, "hipMalloc(mel chain rows)"); }
+  }
+  if (p->n == 2048) {
+    e = hipMalloc(reinterpret_cast<void**>(&r.pool_ctr), sizeof(uint64_t));
+    if (e != hipSuccess) r.pool_ctr = nullptr;
+    else e = hipMemsetAsync(r.pool_ctr, 0, sizeof(uint64_t), (hipStream_t)stream);
+    if (e != hipSuccess) { undo(); return hip_fail(e, "tail pool counter"); }
+  }
+  p->chain_rings.push_back(r);
+  return MGX_OK;
+}
+
 // mgx_extract_device, and with `done` (the small host path) the launch's completion word; inline_frame
 // (the small path's one frame in host memory) goes into the kernel arguments where the kernel takes it
 // (mgx::launch_extract)
@@ -800,62 +831,39 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
   a.scal_defer = a.need_spectrum && any_scalar && nb >= (uint64_t)grid * 8;
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  // the stream's scratch set (the first launch on a stream allocates it, include/meyda_gpu.h)
+  // the stream's scratch set: allocated whole by the first launch on the stream, whatever its shape, so one
+  // untimed call per stream sets the stream up for every later call (include/meyda_gpu.h)
   mgx_plan::ChainRing* ring = nullptr;
   for (auto& r : p->chain_rings)
     if (r.stream == stream) ring = &r;
   if (!ring) {
-    hipEvent_t done = nullptr;
-    e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
-    if (e != hipSuccess) return hip_fail(e, "hipEventCreate(stream scratch)");
-    p->chain_rings.push_back({stream, nullptr, nullptr, done, nullptr, 0});
+    int rc = add_stream_scratch(p, stream);
+    if (rc) return rc;
     ring = &p->chain_rings.back();
   }
-  if (a.scal_defer) {
-    // kScalWords words for each wave of the largest grid (4 waves per workgroup), allocated by the
-    // first launch on the stream that defers its scalars (a small or time-only launch never does)
-    if (!ring->scal) {
-      e = hipMalloc(reinterpret_cast<void**>(&ring->scal), (size_t)p->grid_cap * 4 * mgx::kScalWords * sizeof(uint64_t));
-      if (e != hipSuccess) {
-        ring->scal = nullptr;
-        return hip_fail(e, "hipMalloc(scalar windows)");
-      }
-    }
-    a.scal_rows = ring->scal;
-  }
-  if (a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) {
-    if (!ring->rows) {
-      // 2 FPW x N/2 floats for each wave of the largest grid (4 waves per workgroup)
-      const size_t bytes = (size_t)p->grid_cap * 4 * 2 * (size_t)(fb / 4) * (size_t)p->L * sizeof(float);
-      e = hipMalloc(reinterpret_cast<void**>(&ring->rows), bytes);
-      if (e != hipSuccess) return hip_fail(e, "hipMalloc(mel chain rows)");
-    }
-    a.chain_rows = ring->rows;
-  }
+  if (a.scal_defer) a.scal_rows = ring->scal;
+  if (a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) a.chain_rows = ring->rows;
   // The tail pool at N = 2048 (the kernels without a frame prefetch; not the reference-order ones): the
   // last pool_pct percent of the groups taken by ticket (kernels.hip; 15 %: -2.7 % per launch against the static
   // shares alone, outputs identical, profiles/r05_tail_pool.txt).
-  uint64_t pool_batches = 0;
   if (p->n == 2048 && !(a.chain_groups > 0 && a.need_spectrum && a.need_mfcc) && p->pool_pct > 0) {
     // (nb here counts groups of 16 frames, the kernel's groups; the pool's tickets are batches of 4 frames)
-    const uint64_t ng_all = nb, pg = ng_all * (uint64_t)p->pool_pct / 100, batches = (nframes + 3) / 4;
-    if (pg > 0 && pg < ng_all) {
-      if (!ring->pool_ctr) {
-        e = hipMalloc(reinterpret_cast<void**>(&ring->pool_ctr), sizeof(uint64_t));
-        if (e == hipSuccess) e = hipMemsetAsync(ring->pool_ctr, 0, sizeof(uint64_t), (hipStream_t)stream);
-        if (e != hipSuccess) return hip_fail(e, "tail pool counter");
-        ring->pool_base = 0;
-      }
+    const uint64_t ng_all = nb, pg = ng_all * (uint64_t)p->pool_pct / 100;
+    if (pg > 0 && pg < ng_all && ring->pool_ctr) {
       a.pool_ctr = ring->pool_ctr;
-      a.pool_base = ring->pool_base;
       a.pool_groups = (uint32_t)pg;
-      pool_batches = batches - (ng_all - pg) * 4;
     }
   }
   // (a launch on the plan's own compute stream records no event: destroy synchronises that
   // stream, and the small host path saves the record's ~1 us per call)
   // (a NULL caller stream is never the plan's: s_comp may not exist yet, and then both are NULL)
   hipEvent_t ring_done = (p->s_comp != nullptr && stream == static_cast<void*>(p->s_comp)) ? nullptr : ring->done;
+  // (a launch captured into a graph records no event either: the graph's replays are the caller's to
+  // wait for before mgx_plan_destroy, as any work it launches on the plan's memory)
+  if (ring_done) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) ring_done = nullptr;
+  }
   if (done) {
     a.done_flag = const_cast<uint32_t*>(done);
     a.done_count = p->d_done_count;
@@ -864,8 +872,6 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
   }
   e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, grid, (hipStream_t)stream, inline_frame);
   if (e != hipSuccess) return hip_fail(e, "extract kernel launch");
-  // (every wave ends on one ticket past the pool: the launch consumes its pool's batches plus one per wave)
-  if (a.pool_groups) ring->pool_base += pool_batches + (uint64_t)grid * 4;
   if (ring_done) {
     e = hipEventRecord(ring_done, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord(mel chain rows)");

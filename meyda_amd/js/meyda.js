@@ -34,12 +34,10 @@
 // undefined global), and get() returns fresh arrays rather than internal buffers.
 const path = require('path');
 
-// Kernel arguments in host memory rather than copied to device memory (the HIP runtime's
-// HIP_FORCE_DEV_KERNARG, read when the runtime loads with the addon; a value the environment already
-// sets is kept): a launch's host call is ~1.4 us shorter, and the real-time path's one-frame call ~0.6 us
-// shorter end to end, although the kernel then reads its arguments over PCIe
-// (tools/ubench/small_latency.hip, profiles/r05_inline_frame.txt).
-if (process.env.HIP_FORCE_DEV_KERNARG === undefined) process.env.HIP_FORCE_DEV_KERNARG = '0';
+// (Loading the module changes nothing outside it, like the reference's constructor: the HIP runtime's
+// settings are the application's. For the real-time path, HIP_FORCE_DEV_KERNARG=0 in the environment
+// that starts the process keeps kernel arguments in host memory -- a ~1.4 us shorter launch call, ~0.6 us
+// per one-frame call end to end; INTEGRATION.md, profiles/r05_inline_frame.txt.)
 const addon = require(process.env.MEYDA_AMD_ADDON ||
   path.join(__dirname, '..', 'addon', 'meyda_napi.node'));
 const FEATURE_INFO = require('./feature-info');

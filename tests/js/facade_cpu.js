@@ -8,6 +8,7 @@ const assert = require('assert');
 const path = require('path');
 const golden = require('./golden');
 const kernargPreset = process.env.HIP_FORCE_DEV_KERNARG;
+const envBefore = Object.assign({}, process.env);
 const Meyda = require(path.join(__dirname, '..', '..', 'meyda_amd', 'js', 'meyda.js'));
 
 const ctx = { sampleRate: 44100 };
@@ -105,9 +106,15 @@ check('bufferSize 1 and 2 construct (isPowerOfTwo accepts them; tables only)', (
   assert.strictEqual(t.barkLimits[24], -1);  // loudness.js:44: normalisedSpectrum.length - 1
 });
 
-check('the facade keeps kernel arguments in host memory unless the environment chose', () => {
-  // (set before the addon loaded the HIP runtime; a value the environment set is left as it was)
-  assert.strictEqual(process.env.HIP_FORCE_DEV_KERNARG, kernargPreset === undefined ? '0' : kernargPreset);
+check('loading the facade and constructing Meyda leave process.env as it was', () => {
+  // (src/meyda.js:17-97: construction has no global side effect beyond its ScriptProcessor; the HIP
+  // runtime's settings, HIP_FORCE_DEV_KERNARG among them, are the application's)
+  assert.strictEqual(process.env.HIP_FORCE_DEV_KERNARG, kernargPreset);
+  const now = Object.assign({}, process.env);
+  // (GLOG_*: set by the ROCm runtime's own librocprofiler-register when the HIP runtime loads, not by this code)
+  const changed = Object.keys(Object.assign({}, now, envBefore))
+    .filter((k) => now[k] !== envBefore[k] && !k.startsWith('GLOG_'));
+  assert.deepStrictEqual(changed, [], 'environment keys changed: ' + changed.join(', '));
 });
 
 console.log('facade_cpu: ' + n + ' checks passed');

@@ -182,10 +182,29 @@ def test_bench_c5_field_shape():
     eight = bench.c5_field(8, 262144, 0.027, 1.35, {"rank0": st, "per_rank_period_ms": [1.35] * 8}, 20, True)
     assert eight["frames_total"] == 2097152 and eight["gather"]["status"] == "not run"
     assert eight["kernel_ms"] == 1.3
+    shards = 8 * 262144 * 20 / 0.027
     args = types.SimpleNamespace(steps=20, warmup=5, precision="faithful", single_stream=False)
-    line = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, {"launch_alone_mean_ms": 0.6, "launch_serial_ms": 0.6},
+    st1 = {"launch_alone_mean_ms": 0.6, "launch_serial_ms": 0.6}
+    # a gather that has not completed (a deadline printing the line mid-phase, or a failure): C5 has
+    # no gather-inclusive value, the shards' rate beside it
+    line = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, st1,
                             {"status": "ok", "value": 2.8e9}, {"c5": eight})
     assert line["value"] == 3.5e9 and line["c5"]["frames_total"] == 2097152
+    assert line["c5"]["value"] is None and abs(line["c5"]["shards_value"] - shards) < 1e-6 * shards
+    assert "not run" in line["c5"]["value_source"]
+    # BASELINE C5 is "frames sharded across GPUs with RCCL gather": once the gather ran, c5.value is the
+    # gather-inclusive rate and the shards' rate stays beside it
+    eight["gather"].update({"status": "ok", "value": 0.9 * shards})
+    line = bench.build_line(args, 8, "torchrun", [], 262144, 1024, 3.5e9, 10.0, 0.6, st1,
+                            {"status": "ok", "value": 2.8e9}, {"c5": eight})
+    c5 = line["c5"]
+    assert c5["value"] == 0.9 * shards and abs(c5["shards_value"] - shards) < 1e-6 * shards
+    assert abs(c5["gather"]["vs_shards"] - 0.9) < 1e-12 and c5["value_source"].startswith("gather-inclusive")
+    assert line["value"] == 3.5e9  # the headline keeps the shards (SURVEY §7 hard part 5), gather beside it
+    # N = 1: nothing to gather, value = shards_value
+    line1 = bench.build_line(args, 1, "one", [], 262144, 1024, 4.4e8, 10.0, 0.6, st1, None, {"c5": one})
+    assert line1["c5"]["value"] == line1["c5"]["shards_value"] == one["shards_value"]
+    assert line1["c5"]["value_source"].startswith("one GPU")
     p = bench.parse([])
     assert not p.no_c5 and p.c5_frames == 262144 and not p.strict_gather
 

@@ -65,7 +65,8 @@ def test_c5_shard_2048_all_features(capi, oracle_mod):
     assert torch.allclose(rms * rms * n, out["energy"], rtol=1e-12)
     c = out["spectralCentroid"]
     assert torch.all((c > 0) & (c < n // 2))
-    # a second launch is bitwise identical (deterministic, no atomics)
+    # a second launch is bitwise identical (deterministic: the N = 2048 tail pool takes its batches by
+    # ticket, but each batch is computed once by one wave, whichever; tests/test_gpu_pool.py)
     out2 = plan.extract_torch(frames, ["amplitudeSpectrum", "mfcc", "spectralRolloff", "loudness"])
     torch.cuda.synchronize()
     for k in ("amplitudeSpectrum", "mfcc", "spectralRolloff", "loudness.specific"):

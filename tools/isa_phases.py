@@ -12,9 +12,10 @@ from collections import Counter, OrderedDict
 def kernel_lines(path, n, sub):
     # extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME>; sub = SUB or "sub,light,notime"
     flags = [int(v) for v in str(sub).split(",")] + [0, 0, 0, 0]
-    name = "_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb1ELb0ELb%dELb%dELb%dELb%dEEEvNS_10KernelArgsE" % (n, *flags[:4])
+    # extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN, INL = false>
+    name = "_ZN3mgx12_GLOBAL__N_114extract_kernelILi%dELb1ELb0ELb%dELb%dELb%dELb%dELb0EEEv" % (n, *flags[:4])
     lines = open(path).read().split("\n")
-    start = [i for i, l in enumerate(lines) if l.startswith(name + ":")][0]
+    start = [i for i, l in enumerate(lines) if l.startswith(name) and l.split(";")[0].rstrip().endswith(":")][0]
     out = []
     for l in lines[start + 1:]:
         if l.startswith(".Lfunc_end"):
