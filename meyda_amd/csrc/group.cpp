@@ -240,12 +240,12 @@ int ensure(unsigned char** p, uint64_t* cap, uint64_t bytes, const char* what) {
 // every chunk through CUDA-style IPC instead of RCCL. The ranks rendezvous on a POSIX shared-memory
 // mailbox named by the group id (mgx_comm_unique_id writes that name in place of an RCCL id in this
 // mode); each peer publishes the hipIpcMemHandle of its transfer buffer there, the root opens it
-// (hipIpcOpenMemHandle) and copies each posted chunk into its staging slot on its communication
-// stream, ahead of the same unpack as the RCCL path. Per peer and transfer slot the mailbox holds
-// two sequence numbers: `posted` (the peer's extraction of the slot's chunk has completed) and
-// `consumed` (the root's copy out of it has completed), which stand in for the completion of an
-// ncclSend / ncclRecv pair. The hand-over waits on the host (a rehearsal transport: the shard,
-// chunk, slot and unpack code of the multi-rank path across processes, on one GPU).
+// (hipIpcOpenMemHandle) and its unpack kernel (the RCCL path's) reads each posted chunk from the mapped
+// buffer on the root's communication stream. Per peer and transfer slot the mailbox holds two sequence
+// numbers: `posted` (the peer's extraction of the slot's chunk has completed) and `consumed` (the root's
+// reads of it have completed), which stand in for the completion of an ncclSend / ncclRecv pair. The
+// hand-over waits on the host, one chunk behind the extraction on both sides (a rehearsal transport: the
+// shard, chunk, slot and unpack code of the multi-rank path across processes, on one GPU).
 constexpr uint64_t kIpcMagic = 0x6D67782D69706331ull;  // "mgx-ipc1"
 constexpr uint32_t kIpcMaxRanks = 64;
 constexpr char kIpcTag[] = "mgx-ipc:";
@@ -306,6 +306,31 @@ struct IpcLink {
   std::vector<void*> peer_buf;
   std::vector<uint64_t> peer_gen;
   std::vector<uint64_t> peer_seq;  // 2 per peer
+  std::vector<hipEvent_t> copy_ev;  // root: per (peer, slot), the completion of its reads of the slot's chunk
+  std::vector<uint8_t> copy_open;   // ... recorded and not yet marked consumed
+};
+
+// $MGX_GROUP_TRACE=PREFIX: host timestamps (CLOCK_MONOTONIC, shared by the processes of a host) of every step
+// of a group call's hand-over, appended to PREFIX.<rank> when the call returns (tools/gather_trace.py).
+struct GroupTrace {
+  struct Ev { uint64_t ns; uint32_t chunk, peer; const char* tag; };
+  std::vector<Ev> ev;
+  const char* prefix = getenv("MGX_GROUP_TRACE");
+  void operator()(const char* tag, uint32_t chunk = 0, uint32_t peer = 0) {
+    if (!prefix) return;
+    ev.push_back({(uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                      std::chrono::steady_clock::now().time_since_epoch()).count(), chunk, peer, tag});
+  }
+  void flush(uint32_t rank) {
+    if (!prefix || ev.empty()) return;
+    char path[512];
+    snprintf(path, sizeof path, "%s.%u", prefix, rank);
+    if (FILE* f = fopen(path, "a")) {
+      for (const Ev& e : ev) fprintf(f, "%llu %u %s %u %u\n", (unsigned long long)e.ns, rank, e.tag, e.chunk, e.peer);
+      fclose(f);
+    }
+    ev.clear();
+  }
 };
 
 // How a peer's chunk reaches the root's staging slot.
@@ -389,6 +414,10 @@ int ipc_join(mgx_group* g, const char* id, uint32_t rank) {
 
 void ipc_leave(mgx_group* g) {
   IpcLink& L = g->ipc;
+  for (hipEvent_t e : L.copy_ev)
+    if (e) (void)hipEventDestroy(e);
+  L.copy_ev.clear();
+  L.copy_open.clear();
   for (void* b : L.peer_buf)
     if (b) (void)hipIpcCloseMemHandle(b);
   L.peer_buf.clear();
@@ -428,15 +457,22 @@ int ipc_post(mgx_group* g, Member& m, int sl) {
   return MGX_OK;
 }
 
-// The root: peer p's chunk of slot sl into `dst` (bytes, 0 for an empty chunk) on its communication
-// stream, once posted; marks it consumed when the copy has completed.
-int ipc_take(mgx_group* g, Member& root, uint32_t p, int sl, unsigned char* dst, uint64_t slot, uint64_t bytes) {
+// The root: peer p's chunk of slot sl, once posted (ipc_take_start: a host wait for the post, the peer's transfer
+// buffer mapped when it is new). The unpack kernel then reads the chunk straight from the peer's mapped buffer
+// (*src; $MGX_IPC_COPY=1: copied into the root's staging slot `dst` first, round 5's form) -- on one device the
+// mapping is the same HBM, and a hipMemcpyAsync out of an IPC mapping takes the runtime's peer-copy path, ~0.5 ms
+// per 52 MB step on the rehearsal box (profiles/r06_gather_breakdown.txt). ipc_take_mark records when the
+// root's reads of the slot are done; ipc_take_finish, later, waits for that and marks the slot consumed so the
+// peer may reuse it. Between the two the root enqueues its next chunk.
+int ipc_take_start(mgx_group* g, uint32_t p, int sl, unsigned char* dst, uint64_t slot, uint64_t bytes, hipStream_t s,
+                   unsigned char** src) {
   IpcLink& L = g->ipc;
   IpcRankBox& box = L.mail->r[p];
   uint64_t& want = L.peer_seq[2 * (size_t)p + sl];
   ++want;
   if (!ipc_wait([&] { return ld_acq(&box.posted[sl]) >= want; }, ipc_timeout_s()))
     return fail(MGX_E_DEVICE, "root: rank %u never posted chunk %llu of slot %d", p, (unsigned long long)want, sl);
+  *src = dst;
   if (bytes) {
     const uint64_t gen = ld_acq(&box.gen);
     if (gen != L.peer_gen[p]) {  // the peer (re)allocated its transfer buffer: map the new one
@@ -445,13 +481,34 @@ int ipc_take(mgx_group* g, Member& root, uint32_t p, int sl, unsigned char* dst,
       HIP_OK(hipIpcOpenMemHandle(&L.peer_buf[p], box.handle, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
       L.peer_gen[p] = gen;
     }
-    HIP_OK(hipMemcpyAsync(dst, static_cast<unsigned char*>(L.peer_buf[p]) + sl * slot, bytes, hipMemcpyDeviceToDevice,
-                          root.s_comm),
-           "hipMemcpyAsync(ipc chunk)");
-    HIP_OK(hipEventRecord(root.ev_comm_done, root.s_comm), "hipEventRecord");
-    HIP_OK(hipEventSynchronize(root.ev_comm_done), "hipEventSynchronize(ipc chunk)");
+    unsigned char* peer = static_cast<unsigned char*>(L.peer_buf[p]) + sl * slot;
+    const char* cp = getenv("MGX_IPC_COPY");
+    if (cp && atoi(cp) != 0) HIP_OK(hipMemcpyAsync(dst, peer, bytes, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(ipc chunk)");
+    else *src = peer;
   }
-  st_rel(&box.consumed[sl], want);
+  return MGX_OK;
+}
+
+int ipc_take_mark(mgx_group* g, uint32_t p, int sl, hipStream_t s) {
+  IpcLink& L = g->ipc;
+  const size_t k = 2 * (size_t)p + sl;
+  if (L.copy_ev.size() < 2 * (size_t)g->nranks) {
+    L.copy_ev.resize(2 * (size_t)g->nranks, nullptr);
+    L.copy_open.resize(2 * (size_t)g->nranks, 0);
+  }
+  if (!L.copy_ev[k]) HIP_OK(hipEventCreateWithFlags(&L.copy_ev[k], hipEventDisableTiming), "hipEventCreate(ipc take)");
+  HIP_OK(hipEventRecord(L.copy_ev[k], s), "hipEventRecord(ipc take)");
+  L.copy_open[k] = 1;
+  return MGX_OK;
+}
+
+int ipc_take_finish(mgx_group* g, uint32_t p, int sl) {
+  IpcLink& L = g->ipc;
+  const size_t k = 2 * (size_t)p + sl;
+  if (k >= L.copy_open.size() || !L.copy_open[k]) return MGX_OK;
+  HIP_OK(hipEventSynchronize(L.copy_ev[k]), "hipEventSynchronize(ipc chunk)");
+  L.copy_open[k] = 0;
+  st_rel(&L.mail->r[p].consumed[sl], L.peer_seq[k]);
   return MGX_OK;
 }
 
@@ -763,6 +820,68 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
     if (e_end != ncclSuccess) return rccl_fail(e_end, "ncclGroupEnd");
     return MGX_OK;
   };
+  GroupTrace trace;
+  trace("call", nch, (uint32_t)N);  // (chunks, bufferSize)
+  // ($MGX_IPC_SYNC=1, for tools/gather_trace.py: round 5's hand-over, each chunk posted and taken as soon as it
+  // is enqueued, the host waiting for it before the next chunk is enqueued)
+  const bool ipc_sync = ipc && getenv("MGX_IPC_SYNC") && atoi(getenv("MGX_IPC_SYNC")) != 0;
+  // scatter each peer's chunk c (staging slot c & 1) into the root's outputs, on its communication
+  // stream (ordered after the receive / copy into that slot)
+  auto unpack = [&](Member& m, uint32_t c, unsigned char* const* srcs = nullptr) -> int {
+    for (uint32_t p = 1; p < R; ++p) {
+      uint64_t c0, cn;
+      chunk_of(counts[p], nch, c, &c0, &cn);
+      if (!cn) continue;
+      uint64_t off[kFields];
+      packed_layout(d, mask, cn, off);
+      mgx::UnpackArgs ua{};
+      ua.src = srcs ? srcs[p] : m.xfer + ((uint64_t)(p - 1) * 2 + (c & 1)) * slot;
+      mgx_outputs dst = offset_outputs(d, *root_out, mask, start[p] + c0);
+      for (int i = 0; i < kFields; ++i) {
+        if (off[i] == UINT64_MAX) continue;
+        ua.src_off[ua.nseg] = off[i];
+        ua.dst[ua.nseg] = field_ptr(dst, i);
+        ua.dwords[ua.nseg] = field_bytes(d, i) * cn / 4;
+        ++ua.nseg;
+      }
+      HIP_OK(mgx::launch_unpack(ua, m.s_comm), "unpack kernel launch");
+    }
+    return MGX_OK;
+  };
+  // (IPC, the root) every peer's chunk c: taken into its staging slot once posted, then scattered
+  auto ipc_take_all = [&](uint32_t c) -> int {
+    Member& root = g->m[0];
+    HIP_OK(hipSetDevice(root.device), "hipSetDevice");
+    trace("take_wait", c);
+    std::vector<unsigned char*> srcs(R, nullptr);
+    for (uint32_t p = 1; p < R; ++p) {
+      uint64_t c0, cn;
+      chunk_of(counts[p], nch, c, &c0, &cn);
+      unsigned char* dst = root.xfer + ((uint64_t)(p - 1) * 2 + (c & 1)) * slot;
+      if (int rc = ipc_take_start(g, p, (int)(c & 1), dst, slot, cn ? packed_layout(d, mask, cn, nullptr) : 0, root.s_comm,
+                                  &srcs[p]))
+        return rc;
+      trace("taken", c, p);
+    }
+    if (int rc = unpack(root, c, srcs.data())) return rc;
+    for (uint32_t p = 1; p < R; ++p)
+      if (int rc = ipc_take_mark(g, p, (int)(c & 1), root.s_comm)) return rc;
+    trace("unpacked", c);
+    return MGX_OK;
+  };
+  // ... and chunk c's copies marked consumed once complete
+  auto ipc_finish_all = [&](uint32_t c) -> int {
+    trace("fin_wait", c);
+    for (uint32_t p = 1; p < R; ++p)
+      if (int rc = ipc_take_finish(g, p, (int)(c & 1))) return rc;
+    trace("consumed", c);
+    return MGX_OK;
+  };
+  struct TraceFlush {
+    GroupTrace& t;
+    uint32_t rank;
+    ~TraceFlush() { t.flush(rank); }
+  } trace_flush{trace, g->m[0].rank};
   for (uint32_t c = 0; c < nch; ++c) {
     const int sl = (int)(c & 1);
     // extraction of chunk c on every local rank
@@ -779,9 +898,12 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
           int rc = mgx_extract_device(m.plan, src, cn, &o, st);
           if (rc) return rc;
         }
+        trace("enq", c);
       } else {
         if (ipc) {  // the root has copied the slot's previous chunk out (the mailbox's `consumed`)
+          trace("slot_wait", c);
           if (int rc = ipc_wait_consumed(g, m.rank, sl)) return rc;
+          trace("slot_free", c);
         } else if (c >= 2 || m.xfer_sent[sl]) {
           HIP_OK(hipStreamWaitEvent(st, m.ev_sent[sl], 0), "hipStreamWaitEvent");
         }
@@ -792,25 +914,34 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
         }
         HIP_OK(hipEventRecord(m.ev_comp[sl], st), "hipEventRecord");
         HIP_OK(hipStreamWaitEvent(m.s_comm, m.ev_comp[sl], 0), "hipStreamWaitEvent");
-        if (ipc) {  // posted once extracted (every chunk, an empty one too: the sequence stays aligned)
-          if (int rc = ipc_post(g, m, sl)) return rc;
+        trace("enq", c);
+        // posted once extracted (every chunk, an empty one too: the sequence stays aligned), one chunk
+        // late: chunk c is enqueued before the host waits for chunk c - 1, so the device never idles on it
+        if (ipc && (ipc_sync || c >= 1)) {
+          const uint32_t pc = ipc_sync ? c : c - 1;
+          trace("post_wait", pc);
+          if (int rc = ipc_post(g, m, (int)(pc & 1))) return rc;
+          trace("posted", pc);
         }
       }
     }
     if (R == 1) continue;
     if (ipc) {
-      // the root takes every peer's posted chunk into its staging slot (the other ranks' part of
-      // the transfer was their post above)
+      // the root, one chunk behind its own extraction: marks chunk c - 2's copies consumed (their slots go
+      // back to the peers), takes chunk c - 1 from every peer and scatters it
       Member& root = g->m[0];
-      if (root.rank == 0) {
-        HIP_OK(hipSetDevice(root.device), "hipSetDevice");
-        for (uint32_t p = 1; p < R; ++p) {
-          uint64_t c0, cn;
-          chunk_of(counts[p], nch, c, &c0, &cn);
-          unsigned char* dst = root.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot;
-          if (int rc = ipc_take(g, root, p, sl, dst, slot, cn ? packed_layout(d, mask, cn, nullptr) : 0)) return rc;
+      if (root.rank == 0 && ipc_sync) {
+        if (int rc = ipc_take_all(c)) return rc;
+        if (int rc = ipc_finish_all(c)) return rc;
+      } else if (root.rank == 0) {
+        if (c >= 2) {
+          if (int rc = ipc_finish_all(c - 2)) return rc;
+        }
+        if (c >= 1) {
+          if (int rc = ipc_take_all(c - 1)) return rc;
         }
       }
+      continue;
     } else if (g->loopback()) {
       // the test transports: each peer's chunk into the root's staging slot on the root's
       // communication stream, after the peer's extraction of it -- a device copy, or an RCCL
@@ -877,25 +1008,23 @@ static int group_extract(mgx_group* g, const float* const* frames, const uint64_
         }
         continue;
       }
-      // scatter each peer's chunk into the root's outputs (ordered after its receive)
-      for (uint32_t p = 1; p < R; ++p) {
-        uint64_t c0, cn;
-        chunk_of(counts[p], nch, c, &c0, &cn);
-        if (!cn) continue;
-        uint64_t off[kFields];
-        packed_layout(d, mask, cn, off);
-        mgx::UnpackArgs ua{};
-        ua.src = m.xfer + ((uint64_t)(p - 1) * 2 + sl) * slot;
-        mgx_outputs dst = offset_outputs(d, *root_out, mask, start[p] + c0);
-        for (int i = 0; i < kFields; ++i) {
-          if (off[i] == UINT64_MAX) continue;
-          ua.src_off[ua.nseg] = off[i];
-          ua.dst[ua.nseg] = field_ptr(dst, i);
-          ua.dwords[ua.nseg] = field_bytes(d, i) * cn / 4;
-          ++ua.nseg;
-        }
-        HIP_OK(mgx::launch_unpack(ua, m.s_comm), "unpack kernel launch");
-      }
+      if (int rc = unpack(m, c)) return rc;
+    }
+  }
+  if (ipc && !ipc_sync) {
+    // the last chunk: the peers post it, the root finishes the hand-over (every slot consumed when the
+    // call returns, so a peer's next call never waits on this one)
+    for (Member& m : g->m) {
+      if (m.rank == 0) continue;
+      trace("post_wait", nch - 1);
+      if (int rc = ipc_post(g, m, (int)((nch - 1) & 1))) return rc;
+      trace("posted", nch - 1);
+    }
+    if (g->m[0].rank == 0) {
+      int rc = nch >= 2 ? ipc_finish_all(nch - 2) : MGX_OK;
+      if (!rc) rc = ipc_take_all(nch - 1);
+      if (!rc) rc = ipc_finish_all(nch - 1);
+      if (rc) return rc;
     }
   }
   // the callers' streams (or the members' own) wait for the odd chunks and the gather

@@ -766,22 +766,26 @@ __device__ __forceinline__ FrameRec& rec_at(FrameRec* recs, int fb) {
   return *reinterpret_cast<FrameRec*>(reinterpret_cast<unsigned char*>(recs) + __umul24((unsigned)fb, (unsigned)sizeof(FrameRec)));
 }
 
-// Math.pow(x, 0.23) rounded to float32 (loudness.js:62), without the f64 exp/log
-// routines: x = m 2^e with m in [1, 2); log2 m = log2(m_hi) + m_lo / (m_hi ln 2) from the
-// f32 hardware log (m_hi = (float)m); y = 0.23 log2 x in double; 2^y = 2^floor(y) 2^frac(y)
-// with the f32 hardware exp2 on [0, 1). Relative error ~1e-7 (a float32 ulp or two).
+// Math.pow(x, 0.23) rounded to float32 (loudness.js:62), without the f64 exp/log routines: x = m 2^e with m in
+// [0.5, 1); log2 m from the f32 hardware log of (float)m (the rounding of m moves log2 m by < 2^-24 / ln 2);
+// 0.23 e = q + r / 100 exactly in integers (23 e = 100 q + r, 0 <= r < 100), so y = 0.23 log2 x = q + f with
+// f = r / 100 + 0.23 log2 m in float32 (|error| < 1e-7), and 2^y = 2^q 2^f from the f32 hardware exp2.
+// Relative error ~1.2e-7 (a float32 ulp or two).
 __device__ __forceinline__ float pow023(double x) {
   // 0, inf, NaN (a band sum is never negative): pow's values, without the library routine
   // (its f64 log/exp code would run for a whole wave whenever one band of a frame is silent)
   if (!(x > 0.0 && x < __builtin_huge_val())) return x == 0.0 ? 0.0f : x > 0.0 ? __builtin_huge_valf() : (float)x;
-  int e;
-  const double m = 2.0 * frexp(x, &e);  // [1, 2)
-  const float mh = (float)m, ml = (float)(m - (double)mh);
-  // (the correction ml / (mh ln 2) is ~2^-24 relative: a hardware reciprocal suffices)
-  const float l2m = __builtin_fmaf(ml * 1.4426950408889634f, __builtin_amdgcn_rcpf(mh), __builtin_amdgcn_logf(mh));
-  const double y = 0.23 * ((double)(e - 1) + (double)l2m);
-  const double n = floor(y);
-  return ldexpf(__builtin_amdgcn_exp2f((float)(y - n)), (int)n);
+  const int e = __builtin_amdgcn_frexp_exp(x);                  // x = m 2^e, m in [0.5, 1); e in [-1073, 1024]
+  const float l2m = __builtin_amdgcn_logf((float)__builtin_amdgcn_frexp_mant(x));  // [-1, 0]
+  const uint32_t u = (uint32_t)(23 * e + 25000);                 // 23 e + 250 * 100 > 0
+  const uint32_t qq = u / 100u, r = u - 100u * qq;
+  float f = __builtin_fmaf(0.23f, l2m, (float)r * 0.01f);        // (-0.23, 1)
+  int q = (int)qq - 250;
+  if (f < 0.0f) {
+    f += 1.0f;
+    q -= 1;
+  }
+  return ldexpf(__builtin_amdgcn_exp2f(f), q);
 }
 
 // Math.log(x) of a float32, rounded to float32 (mfcc.js:64): ln x = (e + log2 m) ln 2 with
@@ -792,6 +796,42 @@ __device__ __forceinline__ float ln_f32(float x) {
   int e;
   const float m = 2.0f * frexpf(x, &e);
   return (float)(((double)(e - 1) + (double)__builtin_amdgcn_logf(m)) * kLn2);
+}
+
+// Math.log of a float32 in double, rounded to float32 (mfcc.js:64 as the reference-order MFCC runs it), without
+// the library's double-double log for almost every input: x = 2^e m, m in [1, 2) with c the centre of m's 1/64
+// of the range (plan table: 1/c rounded, -ln(1/c)), r = m (1/c) - 1 (|r| <= 2^-7, one rounding), ln(1 + r) to
+// r^6 (truncation < 2^-51.8), y = e ln2 - ln(1/c) + ln(1 + r): |y - ln x| < 2^-50.5 + 2^-52 |y|, and so is the
+// reference's own log (within an ulp). When y +- (2^-50 + 2^-51 |y|) round to one float32, that float is the
+// reference's; otherwise -- and for 0, denormal, infinite or NaN inputs -- the library log decides (rare: the
+// interval straddles a float32 rounding boundary with probability ~2^-27 at |y| ~ 1).
+__device__ __forceinline__ float ref_ln(float v, GTw lt) {
+  const uint32_t b = __builtin_bit_cast(uint32_t, v);
+  const uint32_t ef = b >> 23;  // the exponent field; >= 256 for a negative input
+  float out = 0.0f;
+  bool slow = ef - 1u >= 254u;  // not a positive normal float
+  if (!slow) {
+    const double m = (double)__builtin_bit_cast(float, (b & 0x7FFFFFu) | 0x3F800000u);
+    const double2 t = ld_tw(lt, (int)((b >> 17) & 63u));
+    const double ed = (double)((int)ef - 127);
+    const double r = __builtin_fma(m, t.x, -1.0);
+    double q = __builtin_fma(r, -1.0 / 6.0, 0.2);
+    q = __builtin_fma(r, q, -0.25);
+    q = __builtin_fma(r, q, 1.0 / 3.0);
+    q = __builtin_fma(r, q, -0.5);
+    const double p = __builtin_fma(r * r, q, r);
+    double y = p + t.y;
+    y = __builtin_fma(ed, 1.90821492927058770002e-10, y);  // ln2_lo
+    y = __builtin_fma(ed, 6.93147180369123816490e-01, y);  // ln2_hi (32 significant bits: e ln2_hi exact)
+    const double d = __builtin_fma(__builtin_fabs(y), 0x1p-51, 0x1p-50);
+    const float lo = (float)(y - d), hi = (float)(y + d);
+    out = lo;
+    slow = lo != hi;
+  }
+  if (__ballot(slow)) {
+    if (slow) out = (float)log((double)v);
+  }
+  return out;
 }
 
 // Arguments live in the kernarg segment (constant address space 4: scalar loads).
@@ -1758,7 +1798,7 @@ __device__ __forceinline__ void mfcc_log(KArgs* q, int l2, FrameRec* recs, int l
   const int nfilt = q->nfilt, nfp = (nfilt + 7) & ~7;
   const bool ref_log = CHAIN;  // MGX_FLAG_MFCC_REFERENCE: the double Math.log, then float32
   auto ln1 = [&](float v, int band) {
-    return band < nfilt ? (ref_log ? (float)log((double)v) : ln_f32(v)) : 0.0f;  // padding for dct_sum
+    return band < nfilt ? (ref_log ? ref_ln(v, gbl(q->t.log_tab)) : ln_f32(v)) : 0.0f;  // padding for dct_sum
   };
   for (int i = l2; i < FPW * (nfp / 2); i += 64) {
     const int fb = i & (FPW - 1), band = 2 * (int)((unsigned)i / FPW);  // (i >= 0: unsigned division)

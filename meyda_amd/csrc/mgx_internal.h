@@ -49,6 +49,7 @@ struct DevTables {
   // MGX_FLAG_MFCC_REFERENCE (plan.cpp chain_schedule, kernels.hip mel_chains):
   const uint32_t* chain_ctl; // per 8-step group and lane: row offset, chain start, the finished chain's store
   const double* chain_w;     // per track, the weights of its chains' steps back to back
+  const double2* log_tab;    // 64 x (1/c_k, -ln(1/c_k)), c_k = 1 + (2k + 1)/128: the reference-order MFCC's ln (kernels.hip ref_ln)
   // The workgroup's LDS tables as one image (kernels.hip lds_image_kernel, built once per plan): the bark
   // limits' prefix-row offsets, the staged twiddles and the DCT table, byte for byte as they sit in LDS
   // from Lds<N>::kc_off + 128 on; each launch's prologue copies it in one pass of 16-byte loads.

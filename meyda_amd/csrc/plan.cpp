@@ -643,7 +643,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
                o_kl = carve<int>(off, L),
                o_lim = carve<int>(off, mgx::kBark + 1), o_mw = carve<uint32_t>(off, mrec.size()), o_dct = carve<float>(off, dct.size()),
                o_mb = carve<int32_t>(off, bins.size()), o_cl = carve<uint32_t>(off, cs.ctl.size()),
-               o_cw = carve<double>(off, cs.w.size());
+               o_cw = carve<double>(off, cs.w.size()), o_lt = carve<double>(off, 2 * 64);
   std::vector<unsigned char> host(off, 0);
   auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) memcpy(host.data() + at, src, bytes); };
   put(o_win, d->window == MGX_WINDOW_HAMMING ? ham.data() : han.data(), n * sizeof(float));
@@ -657,6 +657,17 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   put(o_dct, dct.data(), dct.size() * sizeof(float));
   put(o_cl, cs.ctl.data(), cs.ctl.size() * sizeof(uint32_t));
   put(o_cw, cs.w.data(), cs.w.size() * sizeof(double));
+  {
+    // the reference-order MFCC's natural log (kernels.hip ref_ln): per 1/64 of the mantissa range its centre's
+    // reciprocal, rounded, and the negated log of that reciprocal, from the 64-bit-mantissa long double log
+    double lt[2 * 64];
+    for (int k = 0; k < 64; ++k) {
+      const double inv = (double)(1.0L / (1.0L + (long double)(2 * k + 1) / 128.0L));
+      lt[2 * k] = inv;
+      lt[2 * k + 1] = (double)(-logl((long double)inv));
+    }
+    put(o_lt, lt, sizeof lt);
+  }
   e = hipMalloc(reinterpret_cast<void**>(&p->dev), off);
   if (e != hipSuccess) { delete p; return hip_fail(e, "hipMalloc(plan tables)"); }
   e = hipMemcpy(p->dev, host.data(), off, hipMemcpyHostToDevice);
@@ -673,6 +684,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   p->t.dct = reinterpret_cast<const float*>(b + o_dct);
   p->t.chain_ctl = reinterpret_cast<const uint32_t*>(b + o_cl);
   p->t.chain_w = reinterpret_cast<const double*>(b + o_cw);
+  p->t.log_tab = reinterpret_cast<const double2*>(b + o_lt);
   // the workgroup's LDS tables as one image (kernels.hip lds_image_kernel), built here once
   {
     const size_t ib = mgx::lds_image_bytes(n, nc, nf);

@@ -47,7 +47,9 @@ PATCHES = {
                    "  const bool need_prefix = opaque(0);")],
     # MGX_FLAG_MFCC_REFERENCE (CHAIN kernels): the chains skipped (the occupancy / LDS-layout /
     # power-row cost alone)
-    "chain_none": [("        if (q->chain_pair) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);",
+    # (both branches: round 5's patch skipped only the paired form, so the unpaired chains ran in its place)
+    "chain_none": [("        if (q->chain_pair) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);\n"
+                    "        else mel_chains<N, false>(q, opaque(lane), gbl(rows), recs, buf, true);",
                     "        if (opaque(0)) mel_chains<N, true>(q, opaque(lane), gbl(rows), recs, buf, true);")],
     # the power-row stores skipped (the chains read stale rows)
     "chain_norows": [("      for (int c = 0; c < R; ++c) {\n        const float a = amp[pa(c * 64 + lane)];",
@@ -74,6 +76,14 @@ PATCHES = {
     # two workgroup barriers per frame at the mel step (the cost of synchronising the workgroup's
     # four waves once per frame; timing only, the batch size must give every wave the same count)
     "bar2": [("  MGX_MARK(bands_done);\n", "  MGX_MARK(bands_done);\n  if (!CHAIN) { lds_barrier(); lds_barrier(); }\n")],
+    # (CHAIN) the frames loaded like the default kernel's (plain loads instead of non-temporal ones)
+    "chain_plainload": [("  if constexpr (NT) return __builtin_nontemporal_load(p);\n  return *p;",
+                         "  return *p;")],
+    # (CHAIN with paired batches) the pair's first batch's log and DCT skipped too (no_ln / no_dct skip the second's)
+    "chain_nomfcc2": [("        if (CHAIN && q->chain_pair) mfcc_log<CHAIN, SUB>(q, l2, recs, 32);  // the pair's first batch",
+                       "        if (opaque(0) && CHAIN && q->chain_pair) mfcc_log<CHAIN, SUB>(q, l2, recs, 32);"),
+                      ("        if (CHAIN && q->chain_pair) mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 32, f0 - wstride * FPW);",
+                       "        if (opaque(0) && CHAIN && q->chain_pair) mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 32, f0 - wstride * FPW);")],
     "no_mel": [("  } else if (!CHAIN && ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && !CHAIN && ap->need_mfcc) {\n    mel_energies")],
 }
 
