@@ -1097,12 +1097,30 @@ __device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec
   };
   double acc = 0.0;  // the Float32Array element, held exactly in double
   uint32_t c = ctl[lane], cn = ctl[64 + lane];  // (the table has ng + 1 >= 2 rows)
+  // A group's power-row values are loaded one group ahead: their loads issue before the previous group's 8
+  // steps, so the ring's memory latency (it is written to device memory in phase 1 and rarely still in the L2)
+  // overlaps those steps instead of stalling every group. (The weights, a few KB read by every wave, come from
+  // the L2; holding them one group ahead as well took the kernel past 128 VGPRs.)
+  // (N = 256, at 6 waves per SIMD: the second set spilled; it keeps the loads in the group)
+  constexpr bool kAhead = N >= 512;
+  f32x4 p0, p1;
+  if constexpr (kAhead) {
+    const GF4 pr = (GF4)(ring + (c & 0x1FFFu));  // a multiple of 4 floats (chain_schedule)
+    p0 = pr[0];
+    p1 = pr[1];
+  }
   for (int g = 0; g < ng; ++g) {
+    if constexpr (!kAhead) {
+      const GF4 pr = (GF4)(ring + (c & 0x1FFFu));
+      p0 = pr[0];
+      p1 = pr[1];
+    }
+    // (the last group fetches its own row again: a harmless reload in place of a branch)
+    const GF4 prn = (GF4)(ring + ((kAhead && g + 1 < ng ? cn : c) & 0x1FFFu));
+    const f32x4 n0 = kAhead ? prn[0] : p0, n1 = kAhead ? prn[1] : p1;
     double w[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) w[u] = wp[g * 8 + u];
-    const GF4 pr = (GF4)(ring + (c & 0x1FFFu));      // a multiple of 4 floats (chain_schedule)
-    const f32x4 p0 = pr[0], p1 = pr[1];
     const uint32_t cnn = ctl[(g + 2 < ng ? g + 2 : ng) * 64 + lane];
     const float p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
     store(c, acc);  // the chain that ends here (or the scratch word)
@@ -1111,6 +1129,8 @@ __device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec
     acc = (double)(float)(a0 + w[0] * (double)p[0]);
 #pragma unroll
     for (int u = 1; u < 8; ++u) acc = (double)(float)(acc + w[u] * (double)p[u]);  // two roundings, the float32 store
+    p0 = n0;
+    p1 = n1;
     c = cn;
     cn = cnn;
   }
@@ -1814,10 +1834,12 @@ template <bool CHAIN, bool SUB>
 __device__ __forceinline__ void mfcc_dct(KArgs* q, int l2, FrameRec* recs, const float* dct_lds, int lmo, uint64_t fbase) {
   constexpr int FPW = 4;
   const int nc = q->ncoef, nfilt = q->nfilt;
-  if (CHAIN || q->dct_sequential) {
-    // MGX_FLAG_DCT_SEQUENTIAL, and the reference-order MFCC (CHAIN): VALU FMAs in the reference's
-    // sequential order, one lane per (coefficient, frame). (The matrix-core form below is the
-    // default: 0.5 % faster for the whole kernel and equal on every golden coefficient)
+  if (q->dct_sequential) {
+    // MGX_FLAG_DCT_SEQUENTIAL: VALU FMAs in the reference's sequential order, one lane per (coefficient,
+    // frame). The matrix-core form below computes the same sums: v_mfma_f64_4x4x4 adds its four products to
+    // the accumulator one FMA after another in k order (tools/ubench/mfma_f64_order.hip: 128,000 of 128,000
+    // chained outputs bit-equal to the sequential chain), so a chain of steps over ascending band quartets IS
+    // mfcc.js's sequential double sum -- the reference-order MFCC (CHAIN) takes it too.
     for (int i = l2; i < FPW * nc; i += 64) {
       const int c = (int)((unsigned)i / FPW), fb = i & (FPW - 1);
       const uint64_t f = fbase + fb;
@@ -1832,8 +1854,8 @@ __device__ __forceinline__ void mfcc_dct(KArgs* q, int l2, FrameRec* recs, const
   // tools/ubench/mfma_f64_4x4_layout.hip): A[i][k] of block g at lane 16k + 4g + i, B[k][j] at
   // 16k + 4g + j, D[i][j] at 16i + 4g + j. So lane l loads DCT[c = l & 15][band n0 + (l >> 4)] and
   // lm[frame l & 3][band n0 + (l >> 4)], and ends with coefficient 4 ((l >> 2) & 3) + (l >> 4) of
-  // frame l & 3. The products of two floats are exact in double, as in the reference; only the f64
-  // summation order differs.
+  // frame l & 3. The products of two floats are exact in double, and the matrix core adds them in band
+  // order (one FMA per k, see above): the reference's sequential sum, bit for bit.
   static_assert(FPW == 4, "one 4 x 4 block column per frame of the batch");
   const int kk = (l2 >> 4) & 3, fa = l2 & 3, nsteps = (nfilt + 3) >> 2;
   const float* lmrow = rec_at(recs, fa).lm + lmo;

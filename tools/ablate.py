@@ -84,6 +84,12 @@ PATCHES = {
                        "        if (opaque(0) && CHAIN && q->chain_pair) mfcc_log<CHAIN, SUB>(q, l2, recs, 32);"),
                       ("        if (CHAIN && q->chain_pair) mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 32, f0 - wstride * FPW);",
                        "        if (opaque(0) && CHAIN && q->chain_pair) mfcc_dct<CHAIN, SUB>(q, l2, recs, dct_lds, 32, f0 - wstride * FPW);")],
+    # (CHAIN) the chain weights as constants instead of loads (is the chains' cost the weights' load latency?)
+    "chain_wconst": [("    for (int u = 0; u < 8; ++u) w[u] = wp[g * 8 + u];\n    const uint32_t cnn",
+                      "    for (int u = 0; u < 8; ++u) w[u] = 0.125 * (u + 1 + (g & 1));\n    const uint32_t cnn")],
+    # (CHAIN) ... and the power rows as constants too (the chains' arithmetic alone)
+    "chain_rconst": [("    const f32x4 n0 = kAhead ? prn[0] : p0, n1 = kAhead ? prn[1] : p1;",
+                      "    const f32x4 n0 = p0 * 0.5f + 1.0f, n1 = p1 * 0.5f + 1.0f;")],
     "no_mel": [("  } else if (!CHAIN && ap->need_mfcc) {\n    mel_energies", "  } else if (opaque(0) && !CHAIN && ap->need_mfcc) {\n    mel_energies")],
 }
 

@@ -97,6 +97,32 @@ def main():
               % (k, np.median(v), np.min(v), 100 * (np.median(v) / base - 1), F / np.median(v) / 1e3))
     print("event-timed kernel mean (last events round) %.4f ms" % ev_ms)
 
+    # Per launch on the two streams (an extra, untimed pass of the two_streams schedule with an event pair
+    # around every launch): each stream's launch durations, and how far launch k+1 (the other stream) starts
+    # before launch k ends (its overlap into k's drain) -- what bench.py's pipelined period rests on.
+    pe = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    e = torch.cuda.Event()
+    e.record(s0)
+    s1.wait_event(e)
+    for i in range(K):
+        st = s1 if i & 1 else s0
+        pe[i][0].record(st)
+        plan.extract_device(x.data_ptr(), F, o1 if i & 1 else o0, st.cuda_stream)
+        pe[i][1].record(st)
+    torch.cuda.synchronize()
+    t0 = pe[0][0]
+    starts = np.array([t0.elapsed_time(p) for p, _ in pe])
+    ends = np.array([t0.elapsed_time(q) for _, q in pe])
+    dur = ends - starts
+    ov = ends[:-1] - starts[1:]  # > 0: launch k+1 began before launch k ended
+    period = (ends[-1] - starts[0]) / K
+    print("per launch, two streams (event pair around each launch, untimed pass of %d launches):" % K)
+    print("  stream 0 launch %.4f ms (mean of %d), stream 1 %.4f ms (%d); period %.4f ms"
+          % (dur[0::2].mean(), len(dur[0::2]), dur[1::2].mean(), len(dur[1::2]), period))
+    print("  launch k+1 starts before launch k ends by: median %.4f ms, min %.4f, max %.4f (0: no overlap)"
+          % (np.median(ov), ov.min(), ov.max()))
+    print("  first launches: durations %s; overlaps %s" % (np.round(dur[:4], 4).tolist(), np.round(ov[:3], 4).tolist()))
+
 
 if __name__ == "__main__":
     main()
