@@ -286,13 +286,13 @@ struct KlTab {
   __device__ __forceinline__ int operator()(int r) const { return (int)((w[r >> 1] >> (16 * (r & 1))) & 0xFFFFu); }
 };
 
-// A frame sample: read once and never again. Plain loads: non-temporal ones (`nt`) took the
-// HBM-bound time-only features 12 % faster on a 1 GiB batch (5.9 TB/s), but C2's 128 MiB batch
-// 12 % slower (with plain loads it stays resident in the 256 MiB MALL across launches), and
-// made no change where the kernel is VALU-bound.
-// NT: a non-temporal load (the CHAIN kernels' frames: the power-row ring keeps more of the L2;
-// -0.6..-1.2 % per reference-order launch, profiles/r03_mfcc_tracks.txt. The other kernels keep
-// plain loads: C2's batch stays in the MALL between launches, which nt loads lose; profiles/r05_prologue_ab.txt)
+// A frame's samples: read once and never again. A batch larger than the 256 MiB MALL cannot stay
+// resident across launches, and its frames are read with non-temporal loads (KernelArgs::nt_frames,
+// plan.cpp), which keep the L2 for the lines that are read back -- the scalar windows, the CHAIN
+// kernels' power-row ring (always nt: -0.6..-1.2 % per reference-order launch, profiles/r03_mfcc_tracks.txt).
+// The HBM-bound time-only features ran 12 % faster with them on a 1 GiB batch (5.9 TB/s) and the
+// all-feature launch 1.2 % (profiles/r05_prologue_ab.txt); a smaller batch keeps plain loads, because
+// then it stays in the MALL between launches of the same frames (C2's 128 MiB: 12 % slower with nt).
 // A spectrum output element (amplitude, power, complex: 2-8 KB per frame, written once and never
 // read back): a non-temporal store, which streams past the caches instead of filling them (every
 // output at N = 1024: -8.1..-8.8 % per launch; C2's 1 GiB batch -0.7 %, outputs identical; the same
@@ -302,10 +302,20 @@ __device__ __forceinline__ void st_out(P p, float v) {
   __builtin_nontemporal_store(v, p);
 }
 
-template <bool NT = false>
-__device__ __forceinline__ float ld_frame(const __attribute__((address_space(1))) float* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  return *p;
+// (the lane's CH samples of the frame at p; nt: the launch's run-time choice, NT: always. The empty asm
+// statements keep the two branches apart: without them the compiler hoists or sinks the loads of both
+// into one plain load, the non-temporal hint dropped as metadata the two did not share.)
+template <bool NT, int CH>
+__device__ __forceinline__ void ld_frame(float (&xv)[CH], GF p, unsigned lane, bool nt) {
+  if (NT || nt) {
+    if constexpr (!NT) asm volatile("; nt frame");
+#pragma unroll
+    for (int c = 0; c < CH; ++c) xv[c] = __builtin_nontemporal_load(p + (c * 64 + lane));
+    if constexpr (!NT) asm volatile("; nt frame issued");
+  } else {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) xv[c] = p[c * 64 + lane];
+  }
 }
 
 // Static instruction accounting (tools/isa_phases.py): -DMGX_MARKS puts an assembly comment
@@ -1152,7 +1162,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
                                              const int* klim, float (&xn)[Geo<N>::PREFETCH ? Geo<N>::CH : 1],
                                              GF next, const double2* twl, const float (&wreg)[Geo<N>::CH],
-                                             uint32_t blim, float* rows, int it) {
+                                             uint32_t blim, float* rows, int it, bool ntf) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
   constexpr int L = G::L, R = G::R, CH = G::CH;
@@ -1163,10 +1173,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // mid-frame prefetch of the next frame (G::PF == 2), after the mel records are issued
   // (frames without spectral features: right away)
   auto prefetch_next = [&]() {
-    if constexpr (G::PF == 2) {
-#pragma unroll
-      for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN>(next + (c * 64 + (unsigned)lane));
-    }
+    if constexpr (G::PF == 2) ld_frame<CHAIN>(xn, next, (unsigned)lane, ntf);
   };
   // The window: held in registers for the launch at N = 1024 (Geo::WIN_REG); otherwise its
   // table loads are issued before the energy / zcr reductions, so their latency hides behind
@@ -2094,6 +2101,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // Loads are unconditional (the frame index is clamped; results of frames past the end
   // are never stored), so they issue back to back with no branches or waits between them.
   // With G::PREFETCH the next frame of the wave is loaded while this one is processed.
+  const bool ntf = args_ptr()->nt_frames != 0;  // (one scalar register for the launch)
   auto frame_ptr = [&](uint64_t b, int j) {
     uint64_t f = b * FPW + j;
     f = f < nf ? f : nf - 1;
@@ -2102,9 +2110,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     return (GF)uniform_ptr(gbl(base) + f * (uint64_t)N);
   };
   auto load = [&](float (&xv)[CH], uint64_t b, int j) {
-    const GF xin = frame_ptr(b, j);
-#pragma unroll
-    for (int c = 0; c < CH; ++c) xv[c] = ld_frame<CHAIN>(xin + (c * 64 + (unsigned)lane));
+    ld_frame<CHAIN>(xv, frame_ptr(b, j), (unsigned)lane, ntf);
   };
 
   // The workgroup's LDS tables, from the plan's image (lds_image_kernel) in one pass of 16-byte loads,
@@ -2127,9 +2133,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   }
   if constexpr (G::PREFETCH && !INL) {  // (load(xn, b0, 0) with the burst's frame pointer)
     const uint64_t f = b0 * FPW < nf ? b0 * FPW : nf - 1;
-    const GF xin = (GF)uniform_ptr(gbl(frames_p) + f * (uint64_t)N);
-#pragma unroll
-    for (int c = 0; c < CH; ++c) xn[c] = ld_frame<CHAIN>(xin + (c * 64 + (unsigned)lane));
+    ld_frame<CHAIN>(xn, (GF)uniform_ptr(gbl(frames_p) + f * (uint64_t)N), (unsigned)lane, ntf);
   }
   // the output pointers, then the image's chunks
   if (threadIdx.x < MGX_NUM_SCALARS) reinterpret_cast<void**>(smem + LY::kc_off)[threadIdx.x] = kp;
@@ -2217,7 +2221,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       }
       frame_phase1<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
                                       reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
-                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim, rows, it);
+                                      reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim, rows, it, ntf);
     }
     wave_sync();
 

@@ -79,6 +79,7 @@ struct KernelArgs {
   int need_energy;       // rms or energy: the wave sum of the squares (SUB kernel)
   int need_zcr;          // zcr: the sign-change ballots (SUB kernel)
   int scal_defer;        // the scalars by windows (scalar_pass): a spectrum is computed and a scalar requested
+  int nt_frames;         // the frames read with non-temporal loads: the batch is larger than the MALL (kernels.hip ld_frame)
   // Small host batches (plan.cpp extract_host_small): every wave counts itself in done_count at
   // its end, after its output stores are visible to the host, and the last one sets the mapped
   // host word done_flag to done_seq, which the host polls instead of synchronising the stream.

@@ -481,6 +481,9 @@ struct mgx_plan {
   // small host batches (kSmallBatchFrames): pinned, device-mapped, coherent host buffers
   uint64_t small_max = kSmallBatchFrames;
   int pool_pct = 15;  // the N = 2048 tail pool's share of the groups, percent (MGX_POOL_PCT overrides; 0: off)
+  // a launch whose frames exceed this many bytes reads them with non-temporal loads (KernelArgs::nt_frames):
+  // the MALL's 256 MiB (MGX_NT_MIN_MB overrides, in MiB)
+  uint64_t nt_min_bytes = 256ull << 20;
   // the small path's completion word (KernelArgs::done_flag): a mapped host word, the device
   // counter of finished waves and the launch sequence number
   uint32_t* h_done = nullptr;
@@ -636,6 +639,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   }
   if (const char* sb = getenv("MGX_SMALL_BATCH_FRAMES")) p->small_max = (uint64_t)std::max(0, atoi(sb));
   if (const char* pp = getenv("MGX_POOL_PCT")) p->pool_pct = std::min(50, std::max(0, atoi(pp)));
+  if (const char* nm = getenv("MGX_NT_MIN_MB")) p->nt_min_bytes = (uint64_t)std::max(0, atoi(nm)) << 20;
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
@@ -841,6 +845,11 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
   // one pass at the end of each wave lengthens the launch's tail (+1.6 %). Those, and launches
   // without a scalar output, keep the per-batch form.
   a.scal_defer = a.need_spectrum && any_scalar && nb >= (uint64_t)grid * 8;
+  // A batch larger than the MALL is read past the caches: it cannot stay resident between launches, and
+  // its lines would evict the ones the launch reads back (the scalar windows); N = 1024 all features
+  // -1.2 % per launch, the HBM-bound time-only set -12 % (profiles/r05_prologue_ab.txt, r06_nt_frames.txt).
+  // A smaller one keeps plain loads: launches over the same frames then find them in the MALL (C2).
+  a.nt_frames = nframes * (uint64_t)p->n * sizeof(float) > p->nt_min_bytes;
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   // the stream's scratch set: allocated whole by the first launch on the stream, whatever its shape, so one

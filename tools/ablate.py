@@ -27,8 +27,9 @@ PATCHES = {
                    ("  if (kScalDefer && args_ptr()->scal_defer && (it & (kScalBatches - 1)) != 0) {\n    // the wave's last window",
                     "  if (opaque(0) && (it & (kScalBatches - 1)) != 0) {\n    // the wave's last window")],
     # the frame samples from the address instead of HBM (is the frame load's latency exposed?)
-    "no_frame_load": [("  if constexpr (NT) return __builtin_nontemporal_load(p);\n  return *p;",
-                       "  const uint32_t a = (uint32_t)(uintptr_t)p; return (float)((a >> 2) & 1023) * 0x1p-10f - 0.5f;")],
+    "no_frame_load": [("  if (NT || nt) {\n    if constexpr (!NT) asm volatile(\"; nt frame\");\n#pragma unroll\n    for (int c = 0; c < CH; ++c) xv[c] = __builtin_nontemporal_load(p + (c * 64 + lane));",
+                       "  if (true) {\n#pragma unroll\n    for (int c = 0; c < CH; ++c) { const uint32_t a = (uint32_t)(uintptr_t)(p + (c * 64 + lane)); "
+                       "xv[c] = (float)((a >> 2) & 1023) * 0x1p-10f - 0.5f; }")],
     # the per-lane twiddle loads of passes >= 1 made lane-uniform scalar loads
     "twuni": [("""__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
   const GD q = (GD)p;""", """__device__ __forceinline__ double2 ld_tw(GTw p, int i) {
@@ -77,8 +78,7 @@ PATCHES = {
     # four waves once per frame; timing only, the batch size must give every wave the same count)
     "bar2": [("  MGX_MARK(bands_done);\n", "  MGX_MARK(bands_done);\n  if (!CHAIN) { lds_barrier(); lds_barrier(); }\n")],
     # (CHAIN) the frames loaded like the default kernel's (plain loads instead of non-temporal ones)
-    "chain_plainload": [("  if constexpr (NT) return __builtin_nontemporal_load(p);\n  return *p;",
-                         "  return *p;")],
+    "chain_plainload": [("  if (NT || nt) {", "  if (nt) {")],
     # (CHAIN with paired batches) the pair's first batch's log and DCT skipped too (no_ln / no_dct skip the second's)
     "chain_nomfcc2": [("        if (CHAIN && q->chain_pair) mfcc_log<CHAIN, SUB>(q, l2, recs, 32);  // the pair's first batch",
                        "        if (opaque(0) && CHAIN && q->chain_pair) mfcc_log<CHAIN, SUB>(q, l2, recs, 32);"),
