@@ -126,6 +126,16 @@ typedef struct mgx_plan_desc {
                                         bit-identical wherever the power spectrum is; slower, see
                                         DESIGN.md §5.3). Default off: segmented-scan mel sums, float32
                                         hardware log, the matrix-core DCT, all within 1e-5. */
+#define MGX_FLAG_RESIDENT 4u        /* the real-time path (src/meyda.js:69-91, one buffer per call): one-frame
+                                        mgx_extract_host calls are served by one workgroup that stays on the
+                                        device between calls, polling a mailbox in pinned host memory, instead
+                                        of one launch per call. It holds one CU slot and reads the
+                                        mailbox over PCIe (about N x 16 bytes per microsecond) while it waits,
+                                        and ends itself 20 ms after its last call (MGX_RESIDENT_IDLE_MS), on
+                                        the plan's next call of any other kind, or at mgx_plan_destroy. A device
+                                        synchronisation made meanwhile waits for that end. Faithful per-buffer
+                                        plans of N <= 1024 without MGX_FLAG_MFCC_REFERENCE only
+                                        (MGX_E_UNSUPPORTED otherwise). */
 
 typedef struct mgx_plan mgx_plan;
 
@@ -174,7 +184,8 @@ int mgx_extract_device(mgx_plan* plan, const float* frames, uint64_t num_frames,
 
 /* Host batch: frames and outputs in host memory; returns when the outputs are
  * written. Up to 512 frames run one launch over plan-owned pinned host memory
- * (a single frame of N <= 1024 samples inside the kernel arguments); larger
+ * (a single frame of N <= 1024 samples inside the kernel arguments, or with
+ * MGX_FLAG_RESIDENT handed to the plan's resident workgroup); larger
  * batches stage through plan-owned device buffers in chunks. A one-frame call
  * without spectrum outputs may return while the tail of its launch still runs
  * on the plan's stream: later calls on the plan are ordered after it, and

@@ -110,7 +110,7 @@ static int get_str_prop(napi_env env, napi_value obj, const char* name, char* bu
 }
 
 /* opts: { bufferSize, sampleRate, windowingFunction, precision, mode, numMelBands,
- *         numMfccCoeffs, device, scalarF64, dctSequential, devices } */
+ *         numMfccCoeffs, device, scalarF64, dctSequential, mfccReferenceOrder, resident, devices } */
 static int desc_from_opts(napi_env env, napi_value opts, mgx_plan_desc* d) {
   mgx_plan_desc_init(d);
   d->scalar_f64 = 1;
@@ -135,6 +135,7 @@ static int desc_from_opts(napi_env env, napi_value opts, mgx_plan_desc* d) {
   if (get_u32_prop(env, opts, "scalarF64", &u)) d->scalar_f64 = u ? 1 : 0;
   if (get_u32_prop(env, opts, "dctSequential", &u) && u) d->flags |= MGX_FLAG_DCT_SEQUENTIAL;
   if (get_u32_prop(env, opts, "mfccReferenceOrder", &u) && u) d->flags |= MGX_FLAG_MFCC_REFERENCE;
+  if (get_u32_prop(env, opts, "resident", &u) && u) d->flags |= MGX_FLAG_RESIDENT;
   return 1;
 }
 

@@ -40,6 +40,7 @@ EXPORTS = ["mgx_plan_desc_init", "mgx_plan_create", "mgx_plan_destroy", "mgx_pla
 COMM_ID_BYTES = 128
 FLAG_DCT_SEQUENTIAL = 1  # mgx_plan_desc.flags
 FLAG_MFCC_REFERENCE = 2  # mel sums, log and DCT in the reference's own order
+FLAG_RESIDENT = 4  # one-frame host calls served by a workgroup that stays on the device (include/meyda_gpu.h)
 # output selection bits of a group extraction (MGX_OUT_* in include/meyda_gpu.h)
 OUT_LOUDNESS_SPECIFIC, OUT_MFCC, OUT_AMPLITUDE, OUT_POWER, OUT_COMPLEX = (1 << 13, 1 << 14, 1 << 15, 1 << 16,
                                                                           1 << 17)
@@ -167,7 +168,7 @@ def check(rc):
 
 def make_desc(buffer_size=512, sample_rate=44100.0, window="hanning", precision="faithful",
               mode="per_buffer_fft", num_mel_bands=26, num_mfcc_coeffs=13, scalar_f64=False,
-              device=0, dct_sequential=False, mfcc_reference=False):
+              device=0, dct_sequential=False, mfcc_reference=False, resident=False):
     d = PlanDesc()
     lib().mgx_plan_desc_init(ctypes.byref(d))
     d.buffer_size = buffer_size
@@ -179,7 +180,8 @@ def make_desc(buffer_size=512, sample_rate=44100.0, window="hanning", precision=
     d.num_mfcc_coeffs = num_mfcc_coeffs
     d.scalar_f64 = 1 if scalar_f64 else 0
     d.device = device
-    d.flags = (FLAG_DCT_SEQUENTIAL if dct_sequential else 0) | (FLAG_MFCC_REFERENCE if mfcc_reference else 0)
+    d.flags = ((FLAG_DCT_SEQUENTIAL if dct_sequential else 0) | (FLAG_MFCC_REFERENCE if mfcc_reference else 0) |
+               (FLAG_RESIDENT if resident else 0))
     return d
 
 

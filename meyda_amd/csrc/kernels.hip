@@ -1956,6 +1956,49 @@ __device__ __forceinline__ void done_signal(KArgs* q, int lane) {
   }
 }
 
+// MGX_FLAG_RESIDENT: wave 0 of the resident launch reads the whole mailbox (KernelArgs::res_mail) with two
+// reads in flight -- the next issued before the oldest is checked; vector loads return in issue order -- so a
+// posted frame is taken about one PCIe round trip after it lands (tools/ubench/resident_latency.hip: the
+// host's post to its answer 3.1 us at N = 512, against 4.6 with one read at a time and 8.4 for a launch per
+// call that reads the same frame). Lane l reads words 64c + l: the frame's samples land as x[c], the
+// kernel's own layout.
+template <int CH>
+__device__ __forceinline__ void res_issue(uint64_t (&w)[CH], const uint64_t* mail, unsigned lane) {
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+    w[c] = __hip_atomic_load(gbl(mail) + (c * 64 + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// 1: every word carries request seq (its samples into x); -1: word 0 carries the stop word; 0: not yet
+template <int CH>
+__device__ __forceinline__ int res_take(const uint64_t (&w)[CH], uint32_t seq, float (&x)[CH]) {
+  uint32_t bad = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) bad |= (uint32_t)(w[c] >> 32) ^ seq;
+  if ((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(w[0] >> 32)) == kResStop) return -1;
+  if (__ballot(bad != 0)) return 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) x[c] = __uint_as_float((uint32_t)w[c]);
+  return 1;
+}
+// The wait for request seq: true with its frame in x; false on the stop word, or when res_idle ticks of the
+// 100 MHz clock pass without it (every launch ends on its own: a host that stops posting leaves no wave
+// behind for longer than the idle timeout).
+template <int CH>
+__device__ __forceinline__ bool res_wait(const uint64_t* mail, uint32_t seq, uint32_t idle, float (&x)[CH], unsigned lane) {
+  const unsigned long long t0 = wall_clock64();
+  uint64_t a[CH], b[CH];
+  res_issue<CH>(a, mail, lane);
+  for (;;) {
+    res_issue<CH>(b, mail, lane);
+    int r = res_take<CH>(a, seq, x);
+    if (r != 0) return r > 0;
+    res_issue<CH>(a, mail, lane);
+    r = res_take<CH>(b, seq, x);
+    if (r != 0) return r > 0;
+    if (wall_clock64() - t0 > idle) return false;
+  }
+}
+
 #if MGX_WAVE_TIMES
 // (diagnostic build only, tools/wave_times.py) per wave: start, after the prologue, end (the
 // 100 MHz real-time clock) and the CU id / workgroup; and the first wave's phase stamps of its first
@@ -1963,8 +2006,8 @@ __device__ __forceinline__ void done_signal(KArgs* q, int lane) {
 __device__ unsigned long long g_wave_times[65536 * 4];
 #endif
 
-template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN, bool INL = false>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>::WPE))) void extract_kernel(
+template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN, bool INL = false, bool RES = false>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RES ? 1 : Geo<N>::WPE))) void extract_kernel(
     std::conditional_t<INL, KernelArgsInline<N>, KernelArgs> a) {
   using G = Geo<N>;
   using PG = PassGeo<N>;
@@ -2165,6 +2208,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
   // The static batches (stride wstride from b0), then, with a tail pool, batches taken by ticket; a stolen
   // batch does not count in `it` (the scalar windows and pairs follow the static batches only).
   bool stolen = false;
+  // RES: the request the resident launch waits for next, and its frame
+  uint32_t rseq = RES ? args_ptr()->res_seq : 0;
+  float xr[RES ? CH : 1];
   for (uint64_t b = b0;;) {
     if (!stolen && b >= bend) {
       if (!kPool || pool_groups == 0) break;
@@ -2197,6 +2243,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       if (t >= pool) break;
       b = first + t;
     }
+    if constexpr (RES) {
+      // the resident launch (one frame per request, wave 0; the others have no batch): the next request
+      KArgs* q = args_ptr();
+      if (!res_wait<CH>(q->res_mail, rseq, q->res_idle, xr, (unsigned)lane)) break;
+    }
     const uint64_t f0 = b * FPW;
     // ------------------------------------------------------------- phase 1
     for (int j = 0; j < FPW; ++j) {
@@ -2207,7 +2258,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
       if (f >= nf) break;
       float x[CH];
       GF next = nullptr;
-      if constexpr (G::PF == 1) {
+      if constexpr (RES) {
+        // (the frame from the mailbox; the mid-frame prefetch reads a valid table instead, ignored)
+#pragma unroll
+        for (int c = 0; c < CH; ++c) x[c] = xr[c];
+        next = frame_ptr(b, 0);
+      } else if constexpr (G::PF == 1) {
 #pragma unroll
         for (int c = 0; c < CH; ++c) x[c] = xn[c];
         if (j + 1 < FPW) load(xn, b, j + 1);
@@ -2359,6 +2415,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
         prio_lo<4>();
       }
     }
+    if constexpr (RES) {
+      // the request answered: its number released to the completion word after the outputs (the launch does
+      // not end, so its plain stores would otherwise stay in the L2: the host cannot wait on the output words)
+      KArgs* q = args_ptr();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      if (lane == 0) __hip_atomic_store(q->done_flag, rseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ++rseq;
+      continue;
+    }
     if (!stolen) {
       b += wstride;
       ++it;
@@ -2391,7 +2456,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(Geo<N>
     }
   }
   MGX_STAMP(11);
-  if (args_ptr()->done_flag) done_signal(args_ptr(), opaque(lane));
+  if constexpr (RES) {
+    // the resident launch ends (stop word or idle): wave 0 tells the host, after its last outputs
+    if (wave == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      if (lane == 0) __hip_atomic_store(args_ptr()->res_exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  } else if (args_ptr()->done_flag) {
+    done_signal(args_ptr(), opaque(lane));
+  }
   MGX_STAMP(12);
   MGX_CLOCK_STAMP(14);
 #if MGX_WAVE_TIMES
@@ -2463,9 +2536,14 @@ __global__ void unpack_kernel(UnpackArgs a) {
 }
 
 template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false, bool CHAIN = false>
-hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream, const float* inl = nullptr) {
+hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream, const float* inl = nullptr, bool res = false) {
   const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
   if constexpr (N <= kInlineMaxN && FAITH && !LITERAL && !CHAIN) {
+    if (res) {  // MGX_FLAG_RESIDENT: the one-workgroup server of one-frame requests
+      hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN, false, true>), dim3(1), dim3(kThreads), lds,
+                         stream, a);
+      return hipGetLastError();
+    }
     if (inl) {  // the one frame in the kernel arguments (KernelArgsInline<N>)
       KernelArgsInline<N> x;
       x.a = a;
@@ -2514,7 +2592,7 @@ int occupancy_prec(int precision, int mode, int ncoef, int nfilt, bool chain) {
 }
 
 template <int N>
-hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, hipStream_t stream, const float* inl) {
+hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, hipStream_t stream, const float* inl, bool res) {
   if (mode == MGX_MODE_LITERAL) return launch_n<N, true, true>(a, grid, stream);
   if (precision == MGX_PRECISION_FAST) return launch_n<N, false, false>(a, grid, stream);
   const bool every = a.need_mom == 2 && a.need_prefix && a.need_energy && a.need_zcr;
@@ -2529,14 +2607,14 @@ hipError_t launch_prec(int precision, int mode, const KernelArgs& a, int grid, h
   // (LIGHT: a subset reading neither the moments nor the prefix row, e.g. mfcc or the spectra
   // alone, compiled without that code: no runtime branches to keep its registers live)
   if (a.need_spectrum && a.need_mom == 0 && !a.need_prefix)
-    return launch_n<N, true, false, true, true>(a, grid, stream, inl);
+    return launch_n<N, true, false, true, true>(a, grid, stream, inl, res);
   // (NOTIME: every spectral sum but no rms / energy / zcr, e.g. C3: the all-feature schedule
   // with the time-domain reductions compiled out)
   if (a.need_spectrum && a.need_mom == 2 && a.need_prefix && !a.need_energy && !a.need_zcr)
-    return launch_n<N, true, false, false, false, true>(a, grid, stream, inl);
+    return launch_n<N, true, false, false, false, true>(a, grid, stream, inl, res);
   if (a.need_spectrum && !every)
-    return launch_n<N, true, false, true>(a, grid, stream, inl);
-  return launch_n<N, true, false>(a, grid, stream, inl);
+    return launch_n<N, true, false, true>(a, grid, stream, inl, res);
+  return launch_n<N, true, false>(a, grid, stream, inl, res);
 }
 
 template <int N>
@@ -2606,13 +2684,16 @@ int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt, 
 }
 
 hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, int grid,
-                          hipStream_t stream, const float* inline_frame) {
+                          hipStream_t stream, const float* inline_frame, bool resident) {
   if (a.num_frames != 1) inline_frame = nullptr;
+  if (resident && (a.num_frames != 1 || grid != 1 || n > kInlineMaxN || a.res_mail == nullptr || a.res_exit == nullptr ||
+                   a.done_flag == nullptr))
+    return hipErrorInvalidValue;
   switch (n) {
-    case 256: return launch_prec<256>(precision, mode, a, grid, stream, inline_frame);
-    case 512: return launch_prec<512>(precision, mode, a, grid, stream, inline_frame);
-    case 1024: return launch_prec<1024>(precision, mode, a, grid, stream, inline_frame);
-    case 2048: return launch_prec<2048>(precision, mode, a, grid, stream, nullptr);
+    case 256: return launch_prec<256>(precision, mode, a, grid, stream, inline_frame, resident);
+    case 512: return launch_prec<512>(precision, mode, a, grid, stream, inline_frame, resident);
+    case 1024: return launch_prec<1024>(precision, mode, a, grid, stream, inline_frame, resident);
+    case 2048: return launch_prec<2048>(precision, mode, a, grid, stream, nullptr, false);
     default: return hipErrorInvalidValue;
   }
 }

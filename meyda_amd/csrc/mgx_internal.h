@@ -100,7 +100,20 @@ struct KernelArgs {
   // captured into a graph replays with no host state.
   uint64_t* pool_ctr;
   uint32_t pool_groups;
+  // MGX_FLAG_RESIDENT (plan.cpp resident_*): a one-workgroup launch that stays on the device and serves
+  // one-frame requests from a mailbox in mapped host memory, until the host's stop word or res_idle ticks
+  // of the 100 MHz clock without a request. res_mail: N words, (float32 sample bits) | request << 32, each
+  // written by the host with one 8-byte store and read with one 8-byte system-scope load, so a frame is
+  // complete when every word carries the request's number; word 0 carrying kResStop ends the launch.
+  // After each request's outputs the launch releases its number to done_flag (a launch that does not end
+  // leaves plain stores in the L2 until a release writes them back). res_exit: the host word the launch
+  // sets to 1 as it ends.
+  const uint64_t* res_mail;
+  uint32_t* res_exit;
+  uint32_t res_seq;      // the first request number the launch serves
+  uint32_t res_idle;     // idle timeout, ticks of the 100 MHz real-time clock
 };
+constexpr uint32_t kResStop = 0xFFFFFFFFu;  // a request number that stops the resident launch
 
 // A one-frame launch at N <= kInlineMaxN (the real-time path: extract_host_small with one frame) carries
 // its frame in the kernel arguments, after the KernelArgs: the kernel's first loads read it from the
@@ -125,8 +138,11 @@ int hip_fail(hipError_t e, const char* what);
 // inline_frame (host memory, N floats): a one-frame launch at N <= kInlineMaxN passes its frame in the
 // kernel arguments (KernelArgsInline) when a faithful per-buffer kernel without the reference-order
 // chains runs it; a.frames is then not read. Otherwise ignored.
+// resident (MGX_FLAG_RESIDENT, one frame, grid 1, N <= kInlineMaxN, a.res_* set): the launch stays on the
+// device serving requests from a.res_mail until the stop word or the idle timeout (kernels.hip res_wait);
+// the literal, fast and reference-order plans have no resident form (an error).
 hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, int grid,
-                          hipStream_t stream, const float* inline_frame = nullptr);
+                          hipStream_t stream, const float* inline_frame = nullptr, bool resident = false);
 hipError_t launch_synth(float* out, uint64_t count, uint64_t seed, uint64_t first_index,
                         hipStream_t stream);
 hipError_t launch_pcm_decode(const void* pcm, uint64_t count, uint32_t format, uint32_t channels,

@@ -431,7 +431,7 @@ int validate(const mgx_plan_desc* d) {
     return fail(MGX_E_UNSUPPORTED, "num_mel_bands must be in [1, %d]", mgx::kMaxMel);
   if (d->num_mfcc_coeffs < 1 || d->num_mfcc_coeffs > (uint32_t)mgx::kMaxCoeffs)
     return fail(MGX_E_UNSUPPORTED, "num_mfcc_coeffs must be in [1, %d]", mgx::kMaxCoeffs);
-  if (d->flags & ~(MGX_FLAG_DCT_SEQUENTIAL | MGX_FLAG_MFCC_REFERENCE)) return fail(MGX_E_INVALID_ARGUMENT, "unknown plan flags 0x%x", d->flags);
+  if (d->flags & ~(MGX_FLAG_DCT_SEQUENTIAL | MGX_FLAG_MFCC_REFERENCE | MGX_FLAG_RESIDENT)) return fail(MGX_E_INVALID_ARGUMENT, "unknown plan flags 0x%x", d->flags);
   return MGX_OK;
 }
 
@@ -496,11 +496,25 @@ struct mgx_plan {
   float* h_in = nullptr;
   unsigned char* h_out = nullptr;
   size_t h_in_bytes = 0, h_out_bytes = 0;
+  // MGX_FLAG_RESIDENT: one-frame host calls served by a launch that stays on the device (resident_request)
+  bool resident = false;
+  uint32_t res_idle_ms = 20;   // its idle timeout (MGX_RESIDENT_IDLE_MS overrides)
+  hipStream_t s_res = nullptr; // its own stream: nothing else is queued behind it
+  uint64_t* h_mail = nullptr;  // pinned, mapped: N request words (KernelArgs::res_mail), then the exit word
+  uint64_t* d_mail = nullptr;  // the device address of h_mail
+  bool res_live = false;       // a resident launch was started and has not been seen to end
+  uint32_t res_key = 0;        // the outputs it writes (bit k: output k of mgx_outputs requested)
+  uint32_t res_next = 0;       // the request number it waits for next
 };
 
 namespace {
+// resident: the launch is the plan's resident server (MGX_FLAG_RESIDENT), serving requests seq, seq + 1, ...
+struct ResidentLaunch {
+  uint32_t seq;
+};
 int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o, void* stream,
-                        const uint32_t* done, const float* inline_frame = nullptr);
+                        const uint32_t* done, const float* inline_frame = nullptr, const ResidentLaunch* res = nullptr);
+void resident_stop(mgx_plan* p);
 }  // namespace
 
 extern "C" {
@@ -615,8 +629,14 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   const bool pair = chain && nf <= mgx::kChainPairMaxMel;
   if (chain) chain_schedule(bins.data(), nf, L, pair ? 8 : 4, cs);
 
+  if ((d->flags & MGX_FLAG_RESIDENT) && (n > mgx::kInlineMaxN || d->precision != MGX_PRECISION_FAITHFUL ||
+                                         d->mode != MGX_MODE_PER_BUFFER_FFT || chain))
+    return fail(MGX_E_UNSUPPORTED, "MGX_FLAG_RESIDENT: faithful per-buffer plans of N <= %d without MGX_FLAG_MFCC_REFERENCE only",
+                mgx::kInlineMaxN);
+
   auto* p = new mgx_plan();
   p->d = *d;
+  p->resident = (d->flags & MGX_FLAG_RESIDENT) != 0;
   p->n = n;
   p->L = L;
   // spectralSlope.js:9-16 input-independent sums, in the reference's order
@@ -640,6 +660,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   if (const char* sb = getenv("MGX_SMALL_BATCH_FRAMES")) p->small_max = (uint64_t)std::max(0, atoi(sb));
   if (const char* pp = getenv("MGX_POOL_PCT")) p->pool_pct = std::min(50, std::max(0, atoi(pp)));
   if (const char* nm = getenv("MGX_NT_MIN_MB")) p->nt_min_bytes = (uint64_t)std::max(0, atoi(nm)) << 20;
+  if (const char* ri = getenv("MGX_RESIDENT_IDLE_MS")) p->res_idle_ms = (uint32_t)std::min(10000, std::max(1, atoi(ri)));
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
@@ -716,6 +737,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
 int mgx_plan_destroy(mgx_plan* p) {
   if (!p) return MGX_OK;
   (void)hipSetDevice(p->d.device);
+  // the resident launch ends first (its stop word, then its stream)
+  resident_stop(p);
   // every launch that used the plan's memory is done first: the plan's own streams, then the
   // caller streams' scratch events (launches on s_comp record none)
   if (p->s_copy) (void)hipStreamSynchronize(p->s_copy);
@@ -738,6 +761,8 @@ int mgx_plan_destroy(mgx_plan* p) {
   }
   if (p->s_copy) (void)hipStreamDestroy(p->s_copy);
   if (p->s_comp) (void)hipStreamDestroy(p->s_comp);
+  if (p->s_res) (void)hipStreamDestroy(p->s_res);
+  if (p->h_mail) (void)hipHostFree(p->h_mail);
   if (p->h_in) (void)hipHostFree(p->h_in);
   if (p->h_out) (void)hipHostFree(p->h_out);
   if (p->h_done) (void)hipHostFree(p->h_done);
@@ -794,14 +819,16 @@ int add_stream_scratch(mgx_plan* p, void* stream) {
 
 // mgx_extract_device, and with `done` (the small host path) the launch's completion word; inline_frame
 // (the small path's one frame in host memory) goes into the kernel arguments where the kernel takes it
-// (mgx::launch_extract)
+// (mgx::launch_extract); res: the plan's resident launch (resident_request). Any other launch ends the
+// plan's resident one first, so the plan's own work never waits behind it or shares the device with it.
 int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, const mgx_outputs* o, void* stream,
-                        const uint32_t* done, const float* inline_frame) {
+                        const uint32_t* done, const float* inline_frame, const ResidentLaunch* res) {
   if (!p || !o) return fail(MGX_E_INVALID_ARGUMENT, "NULL plan or outputs");
   if (nframes == 0) return MGX_OK;
   if (!frames) return fail(MGX_E_INVALID_ARGUMENT, "frames is NULL");
   if ((o->complex_real == nullptr) != (o->complex_imag == nullptr))
     return fail(MGX_E_INVALID_ARGUMENT, "complex_real and complex_imag must be given together");
+  if (!res) resident_stop(p);
   mgx::KernelArgs a{};
   a.frames = frames;
   a.num_frames = nframes;
@@ -852,6 +879,18 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
   a.nt_frames = nframes * (uint64_t)p->n * sizeof(float) > p->nt_min_bytes;
   hipError_t e = hipSetDevice(p->d.device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if (res) {
+    // the resident launch: one frame per request from the mailbox (the frame pointer only feeds the kernel's
+    // ignored prefetch: a valid table), no stream scratch (one frame: no windows, no pool, no chains)
+    a.frames = p->t.window;
+    a.res_mail = p->d_mail;
+    a.res_exit = reinterpret_cast<uint32_t*>(p->d_mail + p->n);
+    a.res_seq = res->seq;
+    a.res_idle = p->res_idle_ms * 100000u;  // the 100 MHz real-time clock
+    a.done_flag = const_cast<uint32_t*>(done);
+    e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, 1, (hipStream_t)stream, nullptr, true);
+    return e == hipSuccess ? MGX_OK : hip_fail(e, "resident launch");
+  }
   // the stream's scratch set: allocated whole by the first launch on the stream, whatever its shape, so one
   // untimed call per stream sets the stream up for every later call (include/meyda_gpu.h)
   mgx_plan::ChainRing* ring = nullptr;
@@ -954,6 +993,105 @@ size_t out_bytes_per_frame(const mgx_plan* p, const mgx_outputs* o) {
   return per;
 }
 
+// Ends the plan's resident launch if one may be on the device: the stop word into the mailbox's first word
+// (kernels.hip res_take), then its stream (one that already ended on its idle timeout costs only the
+// synchronisation).
+void resident_stop(mgx_plan* p) {
+  if (!p->res_live) return;
+  __atomic_store_n(&p->h_mail[0], (uint64_t)mgx::kResStop << 32, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(p->s_res);
+  p->res_live = false;
+}
+
+// bit k: output k of mgx_outputs requested (the scalars, then loudness, mfcc, amplitude, power, complex)
+uint32_t output_key(const mgx_outputs* o) {
+  uint32_t k = 0;
+  for (int i = 0; i < MGX_NUM_SCALARS; ++i) k |= o->scalars[i] ? 1u << i : 0u;
+  const void* v[] = {o->loudness_specific, o->mfcc, o->amplitude_spectrum, o->power_spectrum, o->complex_real, o->complex_imag};
+  for (int i = 0; i < 6; ++i) k |= v[i] ? 1u << (MGX_NUM_SCALARS + i) : 0u;
+  return k;
+}
+
+// One frame (in p->h_in) through the plan's resident launch (MGX_FLAG_RESIDENT), its outputs landing in the
+// small path's pinned layout h (device addresses d) under request number seq:
+//  * a live launch that writes another output layout, or waits for another request number (a call of
+//    another kind ended it, or the numbers wrapped), is ended first: its kernel arguments fix both;
+//  * the frame goes into the mailbox, each word one 8-byte store tagged with seq (kernels.hip res_wait);
+//  * a launch that ended on its idle timeout is collected, and one is started when none is live -- after
+//    the post, so its first read finds the frame;
+//  * the host spins on the completion word, which the launch releases after each request's outputs (a launch
+//    that does not end leaves its plain stores in the GPU's L2 until a release writes them back: the output
+//    words themselves cannot be waited on as the one-launch path does). A launch that ends while the host
+//    waits (it read the mailbox before the frame landed, then timed out) is started again, twice at most;
+//    past 1 s the call fails with the launch ended.
+int resident_request(mgx_plan* p, const mgx_outputs* o, const mgx_outputs& d, uint32_t seq) {
+  const int n = p->n;
+  hipError_t e = hipSuccess;
+  const uint32_t key = output_key(o);
+  if (p->res_live && (p->res_key != key || p->res_next != seq)) resident_stop(p);
+  if (!p->h_mail) {
+    uint64_t* hm = nullptr;
+    const size_t bytes = (size_t)(n + 8) * sizeof(uint64_t);  // the words, then a 64-byte line for the exit word
+    e = hipHostMalloc(reinterpret_cast<void**>(&hm), bytes, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(resident mailbox)");
+    memset(hm, 0, bytes);
+    e = hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_mail), hm, 0);
+    if (e != hipSuccess) {
+      (void)hipHostFree(hm);
+      return hip_fail(e, "hipHostGetDevicePointer(resident mailbox)");
+    }
+    p->h_mail = hm;
+  }
+  if (!p->s_res) {
+    e = hipStreamCreateWithFlags(&p->s_res, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate(resident)");
+  }
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(p->h_in);
+  for (int i = 0; i < n; ++i) __atomic_store_n(&p->h_mail[i], ((uint64_t)seq << 32) | src[i], __ATOMIC_RELAXED);
+  std::atomic_thread_fence(std::memory_order_release);
+  uint32_t* const exitw = reinterpret_cast<uint32_t*>(p->h_mail + n);
+  auto collect = [&]() -> int {  // the launch has ended (its exit word): its stream, for a fault it may report
+    e = hipStreamSynchronize(p->s_res);
+    p->res_live = false;
+    return e == hipSuccess ? MGX_OK : hip_fail(e, "resident launch");
+  };
+  auto start = [&]() -> int {
+    __atomic_store_n(exitw, 0u, __ATOMIC_RELEASE);
+    const ResidentLaunch rl{seq};
+    const int rc = extract_device_impl(p, p->t.window, 1, &d, p->s_res, p->d_done_map, nullptr, &rl);
+    if (rc) return rc;
+    p->res_live = true;
+    p->res_key = key;
+    return MGX_OK;
+  };
+  int rc = MGX_OK;
+  if (p->res_live && __atomic_load_n(exitw, __ATOMIC_ACQUIRE) != 0) rc = collect();
+  if (!rc && !p->res_live) rc = start();
+  if (rc) return rc;
+  p->res_next = seq + 1;
+  auto landed = [&]() { return __atomic_load_n(p->h_done, __ATOMIC_ACQUIRE) == seq; };
+  const auto t0 = std::chrono::steady_clock::now();
+  int restarts = 0;
+  for (unsigned spins = 0;; ++spins) {
+    if (landed()) break;
+    __builtin_ia32_pause();
+    if ((spins & 63) != 63) continue;
+    const auto now = std::chrono::steady_clock::now();
+    if (__atomic_load_n(exitw, __ATOMIC_ACQUIRE) != 0) {
+      if ((rc = collect())) return rc;
+      if (landed()) break;
+      if (++restarts > 2) return fail(MGX_E_DEVICE, "resident launch: request %u not answered", seq);
+      if ((rc = start())) return rc;
+      continue;
+    }
+    if (now - t0 > std::chrono::seconds(1)) {
+      resident_stop(p);
+      return fail(MGX_E_DEVICE, "resident launch: request %u not answered within 1 s", seq);
+    }
+  }
+  return MGX_OK;
+}
+
 // A small host batch (at most p->small_max frames): the frames into the plan's pinned input
 // buffer, one launch that reads them over PCIe and writes the features into the pinned output
 // buffer, one synchronisation, the features out to the caller's arrays. `fill(dst)` writes the
@@ -975,6 +1113,7 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
   // (a one-frame call may return before its launch has ended (the output words below): nothing may free
   // or reuse the pinned buffers under it)
   if (p->h_in_bytes < in_bytes || p->h_out_bytes < out_bytes) {
+    resident_stop(p);  // (it writes into h_out)
     e = hipStreamSynchronize(p->s_comp);
     if (e != hipSuccess) return hip_fail(e, "small host batch (previous launch)");
   }
@@ -1052,7 +1191,8 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
     p->h_done = hd;
   }
   uint32_t* const ddone = p->d_done_map;
-  p->done_seq = p->done_seq + 1 ? p->done_seq + 1 : 1;  // never 0, the word's initial value
+  // never 0 (the word's initial value) nor the resident launch's stop word
+  p->done_seq = (p->done_seq + 1 == 0 || p->done_seq + 1 == mgx::kResStop) ? 1 : p->done_seq + 1;
   // One frame without spectrum outputs (at most 13 + 24 + 32 words): the host waits on the output words
   // themselves -- each preset to an all-ones NaN and polled until the kernel's store has landed -- and the
   // launch releases no completion word, which spares the system-scope release (a wait for the outputs'
@@ -1060,21 +1200,27 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
   // output that is itself that NaN (a NaN input can carry any payload) only ends the spin at its limit.
   const bool word_wait = nframes == 1 && !o->amplitude_spectrum && !o->power_spectrum && !o->complex_real && !o->complex_imag;
   constexpr uint64_t kSent = ~(uint64_t)0;
-  if (word_wait) {
+  if (word_wait && !(p->resident && nframes == 1)) {
     for (int k = 0; k < MGX_NUM_SCALARS; ++k)
       if (o->scalars[k]) memset(h.scalars[k], 0xFF, ss);
     if (o->loudness_specific) memset(h.loudness_specific, 0xFF, nb * 4);
     if (o->mfcc) memset(h.mfcc, 0xFF, nc * 4);
     std::atomic_thread_fence(std::memory_order_release);
   }
-  // (one frame: also handed over in the kernel arguments, read there by the kernels that take it)
-  rc = extract_device_impl(p, static_cast<const float*>(din), nframes, &d, p->s_comp, word_wait ? nullptr : ddone,
-                           nframes == 1 ? p->h_in : nullptr);
-  if (rc) {
-    (void)hipStreamSynchronize(p->s_comp);
-    return rc;
+  const bool res = p->resident && nframes == 1;
+  if (res) {
+    rc = resident_request(p, o, d, p->done_seq);
+    if (rc) return rc;
+  } else {
+    // (one frame: also handed over in the kernel arguments, read there by the kernels that take it)
+    rc = extract_device_impl(p, static_cast<const float*>(din), nframes, &d, p->s_comp, word_wait ? nullptr : ddone,
+                             nframes == 1 ? p->h_in : nullptr);
+    if (rc) {
+      (void)hipStreamSynchronize(p->s_comp);
+      return rc;
+    }
   }
-  if (word_wait) {
+  if (!res && word_wait) {
     const auto t0 = std::chrono::steady_clock::now();
     bool late = false;
     unsigned spins = 0;
@@ -1104,7 +1250,7 @@ int extract_host_small(mgx_plan* p, uint64_t nframes, const mgx_outputs* o, Fill
   // stream (tools/ubench/small_latency.hip). Past 20 ms (a busy device) the wait blocks on the
   // stream instead, which also reports a failed launch. The spin pauses the core between reads
   // (a contended device leaves N-API worker threads waiting here) and gives up after kSmallSpinUs.
-  if (!word_wait) {
+  if (!res && !word_wait) {
     const auto t0 = std::chrono::steady_clock::now();
     bool seen = false;
     for (unsigned spins = 0;; ++spins) {

@@ -319,6 +319,39 @@ check('addon extractInto: one buffer, caller offsets, equal to extract(); bad of
   addon.destroyPlan(plan);
 });
 
+check('options.resident: per-buffer get() and streaming callbacks equal the launch-per-buffer facade', () => {
+  // include/meyda_gpu.h MGX_FLAG_RESIDENT: the same kernel code on the same frames, byte-identical values
+  const a = new Meyda(ctx, null, 512, null, { resident: true });
+  const b = new Meyda(ctx, null, 512);
+  const same = (x, y, what) => {
+    if (typeof y === 'number') assert.ok(Object.is(x, y), what + ': ' + x + ' vs ' + y);
+    else if (y && y.specific) { same(x.total, y.total, what + '.total'); same(x.specific, y.specific, what + '.specific'); }
+    else for (let k = 0; k < y.length; k++) assert.ok(Object.is(x[k], y[k]), what + '[' + k + ']');
+  };
+  for (let i = 0; i < g.F; i++) {
+    a.process(frameOf(g, i));
+    b.process(frameOf(g, i));
+    for (const list of [['rms', 'spectralCentroid'], ALL]) {
+      const ra = a.get(list), rb = b.get(list);
+      for (const k of list) same(ra[k], rb[k], g.labels[i] + ' ' + k);
+    }
+  }
+  const got = [];
+  const s = new Meyda(ctx, null, 512, (r) => got.push(r), { resident: true });
+  s.start(['rms', 'zcr', 'mfcc']);
+  for (let i = 0; i < 16; i++) s.process(frameOf(g, i));
+  s.stop();
+  assert.strictEqual(got.length, 16);
+  for (let i = 0; i < 16; i++) {
+    b.process(frameOf(g, i));
+    const r = b.get(['rms', 'zcr', 'mfcc']);
+    for (const k of ['rms', 'zcr', 'mfcc']) same(got[i][k], r[k], 'stream ' + i + ' ' + k);
+  }
+  a.dispose();
+  b.dispose();
+  s.dispose();
+});
+
 (async () => {
   for (const [name, fn] of checks) {
     await fn();

@@ -74,6 +74,20 @@ def test_bad_descriptor(capi):
     assert capi.lib().mgx_plan_create(ctypes.byref(d), ctypes.byref(h)) == -3
 
 
+def test_plan_flags_match_header(capi):
+    import ctypes
+    txt = open(os.path.join(ROOT, "include", "meyda_gpu.h")).read()
+    flags = {k: int(v) for k, v in re.findall(r"#define (MGX_FLAG_[A-Z_]+) (\d+)u", txt)}
+    assert flags == {"MGX_FLAG_DCT_SEQUENTIAL": capi.FLAG_DCT_SEQUENTIAL, "MGX_FLAG_MFCC_REFERENCE": capi.FLAG_MFCC_REFERENCE,
+                     "MGX_FLAG_RESIDENT": capi.FLAG_RESIDENT}
+    assert capi.make_desc(resident=True).flags == capi.FLAG_RESIDENT
+    d = capi.make_desc()
+    d.flags = 8  # no such flag: rejected with the descriptor, before any device is touched
+    h = ctypes.c_void_p()
+    assert capi.lib().mgx_plan_create(ctypes.byref(d), ctypes.byref(h)) == -1
+    assert b"unknown plan flags" in capi.lib().mgx_last_error()
+
+
 @pytest.mark.parametrize("n", [512, 1024, 2048])
 def test_host_tables_bit_exact(capi, n):
     g = golden_io.load(n)

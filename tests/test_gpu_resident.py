@@ -1,0 +1,145 @@
+"""MGX_FLAG_RESIDENT: one-frame host calls (the reference's per-buffer path, src/meyda.js:69-91) served by
+one workgroup that stays on the device and polls a mailbox in pinned host memory (kernels.hip res_wait,
+plan.cpp resident_request), against the same plan without the flag (one launch per call).
+
+The resident launch runs the same kernel code on the same frame, so every output must be byte-identical,
+over feature sets that change the output layout (each change ends the launch and starts another), frames
+that are not finite, the completion-word path (spectra), an idle timeout between calls (the launch ends on
+its own and the next call starts one), calls of other kinds in between (they end the launch first), and
+mgx_plan_destroy with a launch still waiting.
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ALL = ["rms", "energy", "zcr", "spectralCentroid", "spectralFlatness", "spectralSlope", "spectralRolloff",
+       "spectralSpread", "spectralSkewness", "spectralKurtosis", "loudness", "perceptualSpread",
+       "perceptualSharpness", "mfcc"]
+SETS = [["rms", "spectralCentroid"], ALL, ["amplitudeSpectrum", "spectralCentroid"], ["zcr"], ["mfcc"],
+        ["powerSpectrum", "loudness"], ["complexSpectrum", "rms"], ["rms", "spectralCentroid"]]
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from meyda_amd import capi
+    if capi.device_count() == 0:
+        pytest.fail("no GPU visible to libmeyda_gpu.so")
+    return capi
+
+
+def frames(n, k, seed=3):
+    rng = np.random.default_rng(seed)
+    fr = list(rng.uniform(-1, 1, (k, n)).astype(np.float32))
+    t = np.arange(n, dtype=np.float32)
+    fr.append(np.sin(2 * np.pi * 440 * t / 44100).astype(np.float32))
+    fr.append(np.zeros(n, np.float32))
+    y = fr[0].copy(); y[5] = np.nan; fr.append(y)
+    y = fr[0].copy(); y[n - 1] = np.inf; fr.append(y)
+    fr.append(np.full(n, 3.0e38, np.float32))
+    fr.append((fr[0] * np.float32(1e-39)).astype(np.float32))
+    return np.stack(fr)
+
+
+def same(a, b, what):
+    assert a.keys() == b.keys(), what
+    for k in a:
+        x, y = np.ascontiguousarray(a[k]), np.ascontiguousarray(b[k])
+        assert x.shape == y.shape and x.dtype == y.dtype, (what, k)
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (what, k, x, y)
+
+
+@pytest.mark.parametrize("n", [256, 512, 1024])
+def test_resident_matches_launch_per_call(capi, n):
+    x = frames(n, 24)
+    ref = capi.Plan(buffer_size=n, scalar_f64=True)
+    res = capi.Plan(buffer_size=n, scalar_f64=True, resident=True)
+    try:
+        for feats in SETS:
+            for i in range(x.shape[0]):
+                same(res.extract(x[i:i + 1], feats), ref.extract(x[i:i + 1], feats), (n, feats, i))
+    finally:
+        res.close()
+        ref.close()
+
+
+def test_resident_float32_scalars_many_calls(capi):
+    # request numbers advance one per call on one live launch; float32 scalar outputs (4-byte output words)
+    n = 512
+    x = frames(n, 500, seed=9)
+    ref = capi.Plan(buffer_size=n)
+    res = capi.Plan(buffer_size=n, resident=True)
+    try:
+        for i in range(x.shape[0]):
+            same(res.extract(x[i:i + 1], ALL), ref.extract(x[i:i + 1], ALL), i)
+    finally:
+        res.close()
+        ref.close()
+
+
+def test_resident_idle_timeout_restart(capi):
+    n = 512
+    x = frames(n, 6, seed=4)
+    old = os.environ.get("MGX_RESIDENT_IDLE_MS")
+    os.environ["MGX_RESIDENT_IDLE_MS"] = "2"
+    try:
+        res = capi.Plan(buffer_size=n, resident=True)
+    finally:
+        if old is None:
+            del os.environ["MGX_RESIDENT_IDLE_MS"]
+        else:
+            os.environ["MGX_RESIDENT_IDLE_MS"] = old
+    ref = capi.Plan(buffer_size=n)
+    try:
+        for i in range(x.shape[0]):
+            for feats in (["rms", "spectralCentroid"], ["amplitudeSpectrum"]):
+                same(res.extract(x[i:i + 1], feats), ref.extract(x[i:i + 1], feats), (i, feats))
+                time.sleep(0.01 if i % 2 else 0.0)  # past the 2 ms timeout every other call
+    finally:
+        res.close()
+        ref.close()
+
+
+def test_resident_between_other_calls(capi):
+    # calls of every other kind on the plan end its resident launch first; one-frame calls then start another
+    import torch
+    n = 1024
+    x = frames(n, 2000, seed=6)
+    ref = capi.Plan(buffer_size=n)
+    res = capi.Plan(buffer_size=n, resident=True)
+    try:
+        same(res.extract(x[:1], ALL), ref.extract(x[:1], ALL), "first")
+        same(res.extract(x[1:65], ALL), ref.extract(x[1:65], ALL), "small batch")
+        same(res.extract(x[2:3], ALL), ref.extract(x[2:3], ALL), "after the small batch")
+        same(res.extract(x, ALL), ref.extract(x, ALL), "staged batch")
+        same(res.extract(x[3:4], ALL), ref.extract(x[3:4], ALL), "after the staged batch")
+        xd = torch.from_numpy(x).cuda()
+        a = res.extract_torch(xd, ALL)
+        b = ref.extract_torch(xd, ALL)
+        torch.cuda.synchronize()
+        same({k: v.cpu().numpy() for k, v in a.items()}, {k: v.cpu().numpy() for k, v in b.items()}, "device batch")
+        same(res.extract(x[4:5], ALL), ref.extract(x[4:5], ALL), "after the device batch")
+    finally:
+        res.close()
+        ref.close()
+
+
+def test_resident_destroy_while_waiting(capi):
+    n = 512
+    x = frames(n, 1)
+    for _ in range(3):
+        res = capi.Plan(buffer_size=n, resident=True)
+        res.extract(x[:1], ["rms", "spectralCentroid"])
+        t0 = time.perf_counter()
+        res.close()  # the stop word, then the launch's stream
+        assert time.perf_counter() - t0 < 0.5
+
+
+@pytest.mark.parametrize("kw", [dict(buffer_size=2048), dict(buffer_size=512, precision="fast"),
+                                dict(buffer_size=512, mode="literal"), dict(buffer_size=512, mfcc_reference=True)])
+def test_resident_unsupported_plans(capi, kw):
+    with pytest.raises(capi.MgxError):
+        capi.Plan(resident=True, **kw)

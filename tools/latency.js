@@ -1,6 +1,7 @@
 'use strict';
 // Real-time path latency of the product's JavaScript facade (meyda_amd/js/meyda.js over the
-// N-API addon and libmeyda_gpu.so; one GPU launch per extraction), for bench.py's `latency`
+// N-API addon and libmeyda_gpu.so; one GPU launch per extraction, or with options.resident one
+// workgroup that stays on the device between buffers), for bench.py's `latency`
 // field (SURVEY.md §8(f) row 1, BASELINE.json configs[0]):
 //   c1: new Meyda(ctx, null, 512).get(['rms', 'spectralCentroid']) on sound1.wav's frame 0
 //       (tests/golden), one process() + get() per call: median / p90 us over >= 1000 calls
@@ -38,11 +39,11 @@ function pct(a, p) {
 const now = () => process.hrtime.bigint();
 const us = (a, b) => Number(b - a) * 1e-3;
 
-function c1() {
+function c1(options) {
   const g = goldenInputs(512);
   const i = g.labels.indexOf('sound1:0');
   const x = g.x.slice(i * 512, (i + 1) * 512);
-  const m = new Meyda(ctx, null, 512);
+  const m = new Meyda(ctx, null, 512, undefined, options);
   let r;
   for (let k = 0; k < 100; k++) {
     m.process(x);
@@ -61,12 +62,12 @@ function c1() {
     rms: r.rms, spectralCentroid: r.spectralCentroid };
 }
 
-function stream(n, feats, K, launches) {
+function stream(n, feats, K, launches, options) {
   const g = goldenInputs(n);
   const frames = [];
   for (let i = 0; i < g.F; i++) frames.push(g.x.slice(i * n, (i + 1) * n));
   let got = 0;
-  const m = new Meyda(ctx, null, n, () => { got++; }, { batchFrames: K });
+  const m = new Meyda(ctx, null, n, () => { got++; }, Object.assign({ batchFrames: K }, options));
   m.start(feats);
   for (let i = 0; i < 50 * K; i++) m.process(frames[i % frames.length]);  // plans, JIT, staging
   m.stop();
@@ -87,14 +88,18 @@ function stream(n, feats, K, launches) {
   m.dispose();
   if (got !== i) throw new Error('callbacks ' + got + ' != buffers ' + i);
   const med = pct(t, 0.5);
-  return { bufferSize: n, batchFrames: K, features: feats, buffers: i, launches: t.length, us_per_launch: med,
+  return { bufferSize: n, batchFrames: K, resident: !!(options && options.resident), features: feats, buffers: i,
+    launches: t.length, us_per_launch: med,
     us_per_buffer: med / K, buffers_per_s: K / (med * 1e-6), us_per_launch_p90: pct(t, 0.9),
     us_per_launch_mean: el / t.length };
 }
 
-const out = { c1: c1(), stream: [] };
+// c1: one launch per buffer (the facade's default); c1_resident: options.resident, the buffers handed to a
+// workgroup that stays on the device (include/meyda_gpu.h MGX_FLAG_RESIDENT)
+const out = { c1: c1(), c1_resident: c1({ resident: true }), stream: [] };
 for (const [n, feats] of [[512, ['rms', 'spectralCentroid']], [1024, ALL]]) {
   for (const K of [1, 64]) out.stream.push(stream(n, feats, K, K === 1 ? 2000 : 300));
+  out.stream.push(stream(n, feats, 1, 2000, { resident: true }));
 }
 out.node = process.version;
 out.cpu_model = os.cpus()[0].model;

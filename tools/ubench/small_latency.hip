@@ -5,6 +5,7 @@
 //   C  an empty kernel + hipStreamSynchronize (the launch and wake-up floor),
 //   E  a busy loop on hipStreamQuery, F  an event and a busy loop on hipEventQuery,
 //   D  the kernel's own duration between two events, G  the same on device-resident frames and outputs,
+//   K  mgx_extract_host on a MGX_FLAG_RESIDENT plan (the frame to a resident workgroup through a mailbox);
 //   H  a kernel that only releases a sequence number to a mapped host word, the host spinning on it (the
 //      protocol's floor), H2 the same with 2,480 bytes of kernel arguments, H3 the same through
 //      hipModuleLaunchKernel with pre-packed arguments, I  mgx_extract_host itself, J  one hipSetDevice call
@@ -217,6 +218,40 @@ int main(int argc, char** argv) {
       th3.push_back(t18 - t17);
     }
   }
+  // K: mgx_extract_host on a plan with MGX_FLAG_RESIDENT (one workgroup stays on the device, polling a mailbox
+  // in pinned host memory): the same frame and features, after the loop above (the launch-per-call plans idle)
+  std::vector<double> tk;
+  double krms[1], kcen[1];
+  {
+    mgx_plan_desc dr = dh;
+    dr.flags |= MGX_FLAG_RESIDENT;
+    mgx_plan* pr = nullptr;
+    if (mgx_plan_create(&dr, &pr) != MGX_OK) {
+      fprintf(stderr, "resident plan: %s\n", mgx_last_error());
+      return 1;
+    }
+    mgx_outputs orr;
+    memset(&orr, 0, sizeof(orr));
+    orr.scalars[MGX_RMS] = krms;
+    orr.scalars[MGX_SPECTRAL_CENTROID] = kcen;
+    for (int it = 0; it < calls + 50; ++it) {
+      const double t0 = now_us();
+      if (mgx_extract_host(pr, hin, 1, &orr) != MGX_OK) {
+        fprintf(stderr, "resident call: %s\n", mgx_last_error());
+        return 1;
+      }
+      const double t1 = now_us();
+      if (it >= 50) tk.push_back(t1 - t0);
+    }
+    if (krms[0] != hrms[0] || kcen[0] != hcen[0]) {
+      fprintf(stderr, "resident outputs differ: %.17g %.17g vs %.17g %.17g\n", krms[0], kcen[0], hrms[0], hcen[0]);
+      return 1;
+    }
+    mgx_plan_destroy(pr);
+  }
+  std::sort(tk.begin(), tk.end());
+  printf("{\"extract_host_resident_us\": %.2f, \"extract_host_resident_p90_us\": %.2f, \"extract_host_resident_min_us\": %.2f}\n",
+         tk[tk.size() / 2], tk[(size_t)(0.9 * (tk.size() - 1))], tk[0]);
   // J: the cost of one hipSetDevice call (the small host path makes two per call)
   double tj0 = now_us();
   for (int i = 0; i < 20000; ++i) CK(hipSetDevice(0));
