@@ -55,6 +55,12 @@ const uint64_t kSmallBatchFrames = 512;
 // How long the small path spins on its completion word before it blocks on the stream (a
 // 512-frame batch takes ~0.1 ms; a longer wait is a busy device, where blocking frees the core).
 const int kSmallSpinUs = 2000;
+// Resident launches (MGX_FLAG_RESIDENT) started and not yet seen to end, per device: each holds one workgroup
+// slot of one CU, so the persistent grid of any other launch on the device is that much smaller (a grid of
+// exactly the resident workgroups would leave one workgroup -- its whole share of the launch -- waiting for a
+// slot until the others finish: twice the launch time).
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_resident_live[kMaxDevices];
 const double kJsPi = 3.141592653589793;        // Math.PI
 const double kJsSqrt1_2 = 0.7071067811865476;  // Math.SQRT1_2
 
@@ -863,7 +869,9 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
   for (int i = 0; i < MGX_NUM_SCALARS; ++i) any_scalar = any_scalar || o->scalars[i];
   const uint64_t fb = (uint64_t)mgx::frames_per_batch(p->n);
   const uint64_t nb = (nframes + fb - 1) / fb;
-  const int grid = (int)std::min<uint64_t>(nb, (uint64_t)p->grid_cap);
+  const int dev_slot = p->d.device >= 0 && p->d.device < kMaxDevices ? p->d.device : 0;
+  const int cap = std::max(1, p->grid_cap - (res ? 0 : g_resident_live[dev_slot].load(std::memory_order_relaxed)));
+  const int grid = (int)std::min<uint64_t>(nb, (uint64_t)cap);
   a.wg_ranks = grid == p->grid_cap && p->cus > 0 ? p->grid_cap / p->cus : 1;
   // The scalars run once per window of a wave's batches (kernels.hip scalar_pass) when the launch
   // computes a spectrum (VALU-bound there: 0.7-1.9 % faster by N, outputs identical) and its waves
@@ -996,11 +1004,16 @@ size_t out_bytes_per_frame(const mgx_plan* p, const mgx_outputs* o) {
 // Ends the plan's resident launch if one may be on the device: the stop word into the mailbox's first word
 // (kernels.hip res_take), then its stream (one that already ended on its idle timeout costs only the
 // synchronisation).
+void resident_ended(mgx_plan* p) {
+  p->res_live = false;
+  g_resident_live[p->d.device >= 0 && p->d.device < kMaxDevices ? p->d.device : 0].fetch_sub(1, std::memory_order_relaxed);
+}
+
 void resident_stop(mgx_plan* p) {
   if (!p->res_live) return;
   __atomic_store_n(&p->h_mail[0], (uint64_t)mgx::kResStop << 32, __ATOMIC_RELEASE);
   (void)hipStreamSynchronize(p->s_res);
-  p->res_live = false;
+  resident_ended(p);
 }
 
 // bit k: output k of mgx_outputs requested (the scalars, then loudness, mfcc, amplitude, power, complex)
@@ -1043,8 +1056,12 @@ int resident_request(mgx_plan* p, const mgx_outputs* o, const mgx_outputs& d, ui
     p->h_mail = hm;
   }
   if (!p->s_res) {
-    e = hipStreamCreateWithFlags(&p->s_res, hipStreamNonBlocking);
-    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate(resident)");
+    // A stream with a CU mask (every CU) gets a hardware queue of its own: the HIP runtime spreads ordinary
+    // streams over a few shared queues, and a queue shared with the resident launch would hold every later
+    // kernel of the other stream behind it until its idle timeout (tests/test_gpu_resident.py).
+    std::vector<uint32_t> mask((size_t)(p->cus + 31) / 32, 0xFFFFFFFFu);
+    e = hipExtStreamCreateWithCUMask(&p->s_res, (uint32_t)mask.size(), mask.data());
+    if (e != hipSuccess) return hip_fail(e, "hipExtStreamCreateWithCUMask(resident)");
   }
   const uint32_t* src = reinterpret_cast<const uint32_t*>(p->h_in);
   for (int i = 0; i < n; ++i) __atomic_store_n(&p->h_mail[i], ((uint64_t)seq << 32) | src[i], __ATOMIC_RELAXED);
@@ -1052,7 +1069,7 @@ int resident_request(mgx_plan* p, const mgx_outputs* o, const mgx_outputs& d, ui
   uint32_t* const exitw = reinterpret_cast<uint32_t*>(p->h_mail + n);
   auto collect = [&]() -> int {  // the launch has ended (its exit word): its stream, for a fault it may report
     e = hipStreamSynchronize(p->s_res);
-    p->res_live = false;
+    resident_ended(p);
     return e == hipSuccess ? MGX_OK : hip_fail(e, "resident launch");
   };
   auto start = [&]() -> int {
@@ -1061,6 +1078,7 @@ int resident_request(mgx_plan* p, const mgx_outputs* o, const mgx_outputs& d, ui
     const int rc = extract_device_impl(p, p->t.window, 1, &d, p->s_res, p->d_done_map, nullptr, &rl);
     if (rc) return rc;
     p->res_live = true;
+    g_resident_live[p->d.device >= 0 && p->d.device < kMaxDevices ? p->d.device : 0].fetch_add(1, std::memory_order_relaxed);
     p->res_key = key;
     return MGX_OK;
   };

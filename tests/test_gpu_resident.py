@@ -143,3 +143,90 @@ def test_resident_destroy_while_waiting(capi):
 def test_resident_unsupported_plans(capi, kw):
     with pytest.raises(capi.MgxError):
         capi.Plan(resident=True, **kw)
+
+
+def test_resident_launch_blocks_no_other_stream(capi):
+    # The resident launch waits on its own hardware queue: work on every other stream of the process -- other
+    # plans, torch's streams -- runs beside it, not after its idle timeout (set long here, so a queue shared
+    # with it would show as seconds).
+    import torch
+    n = 512
+    x = frames(n, 64, seed=8)
+    old = os.environ.get("MGX_RESIDENT_IDLE_MS")
+    os.environ["MGX_RESIDENT_IDLE_MS"] = "3000"
+    try:
+        res = capi.Plan(buffer_size=n, resident=True)
+    finally:
+        if old is None:
+            del os.environ["MGX_RESIDENT_IDLE_MS"]
+        else:
+            os.environ["MGX_RESIDENT_IDLE_MS"] = old
+    others = [capi.Plan(buffer_size=n) for _ in range(3)]
+    try:
+        res.extract(x[:1], ["rms", "spectralCentroid"])  # the resident launch is now waiting
+        took = []
+        for k in range(12):
+            s = torch.cuda.Stream()
+            t0 = time.perf_counter()
+            with torch.cuda.stream(s):
+                y = torch.ones(1 << 20, device="cuda") * 2
+            s.synchronize()
+            took.append(("torch stream %d" % k, time.perf_counter() - t0))
+            assert float(y[0]) == 2.0
+        for i, p in enumerate(others):
+            t0 = time.perf_counter()
+            p.extract(x, ["rms", "spectralCentroid"])
+            p.extract(x[:1], ["rms", "spectralCentroid"])
+            took.append(("plan %d" % i, time.perf_counter() - t0))
+        res.extract(x[1:2], ["rms", "spectralCentroid"])  # still served
+        assert max(t for _, t in took) < 1.0, took
+    finally:
+        res.close()
+        for p in others:
+            p.close()
+
+
+def test_resident_launch_leaves_other_launches_their_speed(capi):
+    # The resident workgroup holds one slot of one CU; a launch of another plan sizes its persistent grid one
+    # workgroup smaller meanwhile (plan.cpp g_resident_live) instead of leaving a workgroup -- its whole share
+    # -- waiting for a slot until the others finish (about twice the launch time).
+    import torch
+    n, F = 1024, 262144
+    xd = torch.empty(F, n, dtype=torch.float32, device="cuda")
+    capi.synth_frames_device(xd, 0x6D657964)
+    big = capi.Plan(buffer_size=n)
+    out, o = big.alloc_outputs(F, ALL)
+
+    def launch_ms(reps=5):
+        s = torch.cuda.current_stream()
+        big.extract_device(xd.data_ptr(), F, o, s.cuda_stream)  # (warm)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ts = []
+        for _ in range(reps):
+            e0.record(s)
+            big.extract_device(xd.data_ptr(), F, o, s.cuda_stream)
+            e1.record(s)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return sorted(ts)[reps // 2]
+
+    alone = launch_ms()
+    old = os.environ.get("MGX_RESIDENT_IDLE_MS")
+    os.environ["MGX_RESIDENT_IDLE_MS"] = "5000"
+    try:
+        res = capi.Plan(buffer_size=512, resident=True)
+    finally:
+        if old is None:
+            del os.environ["MGX_RESIDENT_IDLE_MS"]
+        else:
+            os.environ["MGX_RESIDENT_IDLE_MS"] = old
+    try:
+        x = frames(512, 1)
+        res.extract(x[:1], ["rms"])  # resident from here on
+        beside = launch_ms()
+        res.extract(x[:1], ["rms"])  # still served
+    finally:
+        res.close()
+        big.close()
+    print("launch alone %.4f ms, beside a resident launch %.4f ms" % (alone, beside))
+    assert beside < 1.25 * alone, (alone, beside)

@@ -6,8 +6,8 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O=$R/gpurun_out/res
 mkdir -p $O && cd $R
-timeout -k 10 300 python -u -m pytest tests/test_gpu_resident.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-tail -3 $O/tests.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_resident.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+grep -h 'beside a resident' $O/tests.log; tail -1 $O/tests.log
 timeout -k 10 300 node --expose-gc tests/js/facade_gpu.js > $O/facade.log 2>&1 || { tail -20 $O/facade.log; exit 1; }
 tail -2 $O/facade.log
 timeout -k 10 120 ./tools/ubench/small_latency 512 3000 > $O/small_latency.log 2>&1 || { tail -5 $O/small_latency.log; exit 1; }
