@@ -34,4 +34,4 @@ def test_facade_batched_delivery_host_side():
 @pytest.mark.gpu
 def test_facade_on_gpu():
     out = run_node("facade_gpu.js")
-    assert "facade_gpu: 15 checks passed" in out
+    assert "facade_gpu: 16 checks passed" in out
