@@ -6,6 +6,7 @@
 // golden tests compare them bit-for-bit with the reference's own tables
 // (tests/test_capi_host.py).
 #include <hip/hip_runtime.h>
+#include <emmintrin.h>
 
 #include <cmath>
 #include <cstdarg>
@@ -1063,8 +1064,16 @@ int resident_request(mgx_plan* p, const mgx_outputs* o, const mgx_outputs& d, ui
     e = hipExtStreamCreateWithCUMask(&p->s_res, (uint32_t)mask.size(), mask.data());
     if (e != hipSuccess) return hip_fail(e, "hipExtStreamCreateWithCUMask(resident)");
   }
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(p->h_in);
-  for (int i = 0; i < n; ++i) __atomic_store_n(&p->h_mail[i], ((uint64_t)seq << 32) | src[i], __ATOMIC_RELAXED);
+  // (two words per 16-byte store, the samples interleaved with seq: each aligned 8-byte half is written whole,
+  // which is all the device's word-by-word check needs. Half the stores of word-by-word writes; the call's
+  // time did not move measurably, the device's reads overlap the post.)
+  const float* src = p->h_in;
+  const __m128i sq = _mm_set1_epi32((int)seq);
+  for (int i = 0; i < n; i += 4) {
+    const __m128i xv = _mm_castps_si128(_mm_loadu_ps(src + i));
+    _mm_store_si128(reinterpret_cast<__m128i*>(p->h_mail + i), _mm_unpacklo_epi32(xv, sq));
+    _mm_store_si128(reinterpret_cast<__m128i*>(p->h_mail + i + 2), _mm_unpackhi_epi32(xv, sq));
+  }
   std::atomic_thread_fence(std::memory_order_release);
   uint32_t* const exitw = reinterpret_cast<uint32_t*>(p->h_mail + n);
   auto collect = [&]() -> int {  // the launch has ended (its exit word): its stream, for a fault it may report
