@@ -230,3 +230,23 @@ def test_resident_launch_leaves_other_launches_their_speed(capi):
         big.close()
     print("launch alone %.4f ms, beside a resident launch %.4f ms" % (alone, beside))
     assert beside < 1.25 * alone, (alone, beside)
+
+
+@pytest.mark.parametrize("how", ["exit", "os._exit"])
+def test_resident_process_exit_with_a_live_launch(capi, how):
+    # A process that ends with its resident launch still waiting (no mgx_plan_destroy: os._exit skips every
+    # destructor) ends promptly and cleanly: the launch's idle timeout bounds it either way.
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, os, numpy as np; sys.path.insert(0, %r)\n"
+            "from meyda_amd import capi\n"
+            "p = capi.Plan(buffer_size=512, resident=True)\n"
+            "r = p.extract(np.ones((1, 512), np.float32), ['rms'])\n"
+            "assert abs(float(r['rms'][0]) - 1.0) < 1e-6\n"
+            "sys.stdout.flush()\n"
+            "%s(0)\n") % (root, "sys.exit" if how == "exit" else "os._exit")
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert time.perf_counter() - t0 < 30
