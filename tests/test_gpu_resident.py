@@ -178,6 +178,18 @@ def test_resident_launch_blocks_no_other_stream(capi):
             p.extract(x, ["rms", "spectralCentroid"])
             p.extract(x[:1], ["rms", "spectralCentroid"])
             took.append(("plan %d" % i, time.perf_counter() - t0))
+        # the legacy default stream: a copy and a launch on stream 0 (torch's default stream, and a plan launch
+        # with no stream), each waited for on the host
+        t0 = time.perf_counter()
+        z = (torch.arange(1 << 16, device="cuda", dtype=torch.float32) + 1).cpu()
+        took.append(("default-stream copy", time.perf_counter() - t0))
+        assert float(z[-1]) == float(1 << 16)
+        xd = torch.from_numpy(x).cuda()
+        out, o = others[0].alloc_outputs(x.shape[0], ["rms"])
+        t0 = time.perf_counter()
+        others[0].extract_device(xd.data_ptr(), x.shape[0], o, None)
+        torch.cuda.current_stream().synchronize()
+        took.append(("stream-0 launch", time.perf_counter() - t0))
         res.extract(x[1:2], ["rms", "spectralCentroid"])  # still served
         assert max(t for _, t in took) < 1.0, took
     finally:
