@@ -2247,6 +2247,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RES ? 
       // the resident launch (one frame per request, wave 0; the others have no batch): the next request
       KArgs* q = args_ptr();
       if (!res_wait<CH>(q->res_mail, rseq, q->res_idle, xr, (unsigned)lane)) break;
+      MGX_STAMP(0);  // (the diagnostic build: the request's stamps count from here)
+      MGX_CLOCK_STAMP(13);
     }
     const uint64_t f0 = b * FPW;
     // ------------------------------------------------------------- phase 1
@@ -2419,8 +2421,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RES ? 
       // the request answered: its number released to the completion word after the outputs (the launch does
       // not end, so its plain stores would otherwise stay in the L2: the host cannot wait on the output words)
       KArgs* q = args_ptr();
+      MGX_STAMP(11);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       if (lane == 0) __hip_atomic_store(q->done_flag, rseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      MGX_STAMP(12);
+      MGX_CLOCK_STAMP(14);
       ++rseq;
       continue;
     }

@@ -4,7 +4,9 @@ library (tools/variant.sh wt -DMGX_WAVE_TIMES=1 -> ab/lib_wt.so) stamps the 100 
 at the phases of the first wave's frame (kernels.hip MGX_STAMP); this runs mgx_extract_host on one
 frame many times (the small host path: pinned mapped memory, completion word) and prints, for the
 last calls, the median time from the kernel's first instruction to each stamp, and the call's own
-duration on the host, and the shader clock the launch ran at (clock64 ticks over real time). usage: small_stamps.py LIB [N features ...]"""
+duration on the host, and the shader clock the launch ran at (clock64 ticks over real time). With --resident the
+plan is MGX_FLAG_RESIDENT: the stamps then count from the request's frame taken from the mailbox (stamp 0), the
+last two bracket the completion word's release. usage: small_stamps.py LIB [--resident] [N features ...]"""
 import ctypes
 import json
 import sys
@@ -22,15 +24,17 @@ NAMES = ["start", "prologue barrier", "tables, first load issued", "frame in, wi
 
 
 def main():
-    lib = sys.argv[1]
+    args = [a for a in sys.argv[1:] if a != "--resident"]
+    resident = "--resident" in sys.argv
+    lib = args[0]
     L = ctypes.CDLL(lib)
     L.mgx_plan_create.argtypes = [ctypes.POINTER(capi.PlanDesc), ctypes.POINTER(ctypes.c_void_p)]
     L.mgx_extract_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(capi.Outputs)]
     cases = [(512, ["rms", "spectralCentroid"]), (1024, capi.ALL_FEATURES)]
-    if len(sys.argv) > 2:
-        cases = [(int(sys.argv[2]), sys.argv[3:] or capi.ALL_FEATURES)]
+    if len(args) > 1:
+        cases = [(int(args[1]), args[2:] or capi.ALL_FEATURES)]
     for n, feats in cases:
-        d = capi.make_desc(buffer_size=n, scalar_f64=True)
+        d = capi.make_desc(buffer_size=n, scalar_f64=True, resident=resident)
         h = ctypes.c_void_p()
         assert L.mgx_plan_create(ctypes.byref(d), ctypes.byref(h)) == 0
         x = np.random.default_rng(1).uniform(-1, 1, (1, n)).astype(np.float32)
@@ -43,6 +47,10 @@ def main():
             assert L.mgx_extract_host(h, x.ctypes.data, 1, ctypes.byref(o)) == 0
             calls.append(time.perf_counter() - t0)
             if k >= 1000 and k % 10 == 0:
+                if resident:  # (the launch's last stamps of this request land just after the call returns)
+                    t1 = time.perf_counter()
+                    while time.perf_counter() - t1 < 50e-6:
+                        pass
                 assert L.mgx_debug_stamps(buf) == 0
                 s = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
                 stamps.append((s[:13] - s[0]) * 10e-3)  # 100 MHz ticks -> us
