@@ -1155,8 +1155,10 @@ __device__ __forceinline__ void mel_chains(KArgs* q, int lane, GF ring, FrameRec
   }
 }
 
-// One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks).
-template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN>
+// One frame of phase 1 (wave-level). x holds the raw samples (lane-strided chunks). WREG: the window in
+// wreg (registers loaded once per launch: Geo::WIN_REG, and the resident launches, whose one-frame requests
+// would otherwise each wait for the window's table loads).
+template <int N, bool FAITH, bool LITERAL, bool SUB, bool LIGHT, bool NOTIME, bool CHAIN, bool WREG = Geo<N>::WIN_REG>
 __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], int fb, uint64_t f, bool valid,
                                              int lane, const int (&lp)[Geo<N>::NPASS], const KlTab<N>& kl,
                                              bool dc_lane, float2* buf, double* mom, FrameRec* recs,
@@ -1180,7 +1182,7 @@ __device__ __forceinline__ void frame_phase1(KArgs* ap, float (&x)[Geo<N>::CH], 
   // them rather than at the window step after the reductions' branches (1 % faster at
   // N = 512; a lane-major table read as 16-byte loads was 2-5 % slower at 512 and 2048).
   float wv[CH];
-  if (G::WIN_REG) {
+  if (WREG) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) wv[c] = wreg[c];
   } else if (ap->need_spectrum) {
@@ -2169,7 +2171,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RES ? 
     iv[k] = img[i < nimg ? i : nimg - 1];
   }
   float wreg[CH];
-  if constexpr (G::WIN_REG) {
+  constexpr bool kWinReg = G::WIN_REG || RES;
+  if constexpr (kWinReg) {
     const GF w = gbl(win_p);
 #pragma unroll
     for (int c = 0; c < CH; ++c) wreg[c] = w[c * 64 + lane];
@@ -2277,7 +2280,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RES ? 
       } else {
         load(x, b, j);
       }
-      frame_phase1<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
+      frame_phase1<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN, kWinReg>(args_ptr(), x, j, f, f < nf, lane, lp, kl, dc_lane, buf, mom, recs,
                                       reinterpret_cast<const int*>(smem + LY::kc_off + 16 * 8), xn, next,
                                       reinterpret_cast<const double2*>(smem + LY::twl_off), wreg, blim, rows, it, ntf);
     }
