@@ -230,8 +230,10 @@ def cpu_baseline(n, seconds):
 
 def latency_js():
     """The real-time path through the product's own JS facade over the N-API addon
-    (tools/latency.js): C1's get(['rms','spectralCentroid']) per call, and the start() /
-    process() callback path at batchFrames 1 and 64. A report; never `value`."""
+    (tools/latency.js): C1's get(['rms','spectralCentroid']) per call -- launched per call (`c1`) and
+    served by the resident workgroup (`c1_resident`, options.resident / MGX_FLAG_RESIDENT), back to back and
+    with the host idle 1 ms between calls (`c1_gap`, `c1_resident_gap`) -- and the start() / process()
+    callback path at batchFrames 1 and 64 (and resident). A report; never `value`."""
     import shutil
     import subprocess
     addon = os.path.join(ROOT, "meyda_amd", "addon", "meyda_napi.node")

@@ -17,4 +17,5 @@ grep -v amdgpu.ids $O/latency.log | python3 -c "
 import json,sys
 d=json.loads(sys.stdin.read().strip().splitlines()[-1])
 print('c1', d['c1']['us_per_call'], d['c1']['us_p90'], 'c1_resident', d['c1_resident']['us_per_call'], d['c1_resident']['us_p90'])
+print('c1_gap', d['c1_gap']['us_per_call'], d['c1_gap']['us_p90'], 'c1_resident_gap', d['c1_resident_gap']['us_per_call'], d['c1_resident_gap']['us_p90'])
 for s in d['stream']: print(s['bufferSize'], s['batchFrames'], s['resident'], s['us_per_launch'], s['us_per_buffer'])"

@@ -39,7 +39,7 @@ function pct(a, p) {
 const now = () => process.hrtime.bigint();
 const us = (a, b) => Number(b - a) * 1e-3;
 
-function c1(options) {
+function c1(options, gapUs) {
   const g = goldenInputs(512);
   const i = g.labels.indexOf('sound1:0');
   const x = g.x.slice(i * 512, (i + 1) * 512);
@@ -52,6 +52,10 @@ function c1(options) {
   const t = [];
   const t0 = now();
   while (t.length < 1000 || us(t0, now()) < 2e6) {
+    if (gapUs) {  // the host idle between buffers, as between a real-time source's callbacks
+      const w = now();
+      while (us(w, now()) < gapUs) { /* spin */ }
+    }
     const a = now();
     m.process(x);  // a new buffer: the next get() launches again
     r = m.get(['rms', 'spectralCentroid']);
@@ -96,7 +100,10 @@ function stream(n, feats, K, launches, options) {
 
 // c1: one launch per buffer (the facade's default); c1_resident: options.resident, the buffers handed to a
 // workgroup that stays on the device (include/meyda_gpu.h MGX_FLAG_RESIDENT)
-const out = { c1: c1(), c1_resident: c1({ resident: true }), stream: [] };
+// c1_gap / c1_resident_gap: the same with the host idle 1 ms between calls (a real-time source delivers a buffer
+// every 11.6 ms at 512 samples and 44.1 kHz; the calls are then never back to back)
+const out = { c1: c1(), c1_resident: c1({ resident: true }), c1_gap: c1({}, 1000),
+  c1_resident_gap: c1({ resident: true }, 1000), stream: [] };
 for (const [n, feats] of [[512, ['rms', 'spectralCentroid']], [1024, ALL]]) {
   for (const K of [1, 64]) out.stream.push(stream(n, feats, K, K === 1 ? 2000 : 300));
   out.stream.push(stream(n, feats, 1, 2000, { resident: true }));
