@@ -191,6 +191,7 @@ struct Member {
 int member_init(Member& m, const mgx_plan_desc& d) {
   mgx_plan_desc pd = d;
   pd.device = m.device;
+  pd.flags &= ~MGX_FLAG_RESIDENT;  // (one-frame host calls on one plan: a group's calls never take that path)
   int rc = mgx_plan_create(&pd, &m.plan);
   if (rc) return rc;
   HIP_OK(hipSetDevice(m.device), "hipSetDevice");
