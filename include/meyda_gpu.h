@@ -134,8 +134,8 @@ typedef struct mgx_plan_desc {
                                         and ends itself 20 ms after its last call (MGX_RESIDENT_IDLE_MS), on
                                         the plan's next call of any other kind, or at mgx_plan_destroy. A device
                                         synchronisation made meanwhile waits for that end. Faithful per-buffer
-                                        plans of N <= 1024 without MGX_FLAG_MFCC_REFERENCE only
-                                        (MGX_E_UNSUPPORTED otherwise). */
+                                        plans without MGX_FLAG_MFCC_REFERENCE only (MGX_E_UNSUPPORTED
+                                        otherwise). */
 
 typedef struct mgx_plan mgx_plan;
 

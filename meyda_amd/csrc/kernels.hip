@@ -2090,7 +2090,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RES ? 
   // the launch and the SIMDs ran 3, 2, then 1 wave for the rest (tools/wave_times.py).
   // Rank r takes a share of its own instead (22 / 18 / 14 / 10 of 64 at N = 1024).
   // (the tail pool: the static shares cover the first ng - pool_groups groups, kPool kernels only)
-  constexpr bool kPool = G::PF == 0 && !CHAIN && !INL;
+  constexpr bool kPool = G::PF == 0 && !CHAIN && !INL && !RES;
   const uint64_t ng_all = (nb + 3) / 4;
   const uint64_t pool_groups = kPool ? (uint64_t)args_ptr()->pool_groups : 0;
   const uint64_t ng = ng_all - (pool_groups < ng_all ? pool_groups : ng_all);
@@ -2546,12 +2546,14 @@ __global__ void unpack_kernel(UnpackArgs a) {
 template <int N, bool FAITH, bool LITERAL, bool SUB = false, bool LIGHT = false, bool NOTIME = false, bool CHAIN = false>
 hipError_t launch_n(const KernelArgs& a, int grid, hipStream_t stream, const float* inl = nullptr, bool res = false) {
   const size_t lds = Lds<N>::bytes(a.ncoef, a.nfilt);
-  if constexpr (N <= kInlineMaxN && FAITH && !LITERAL && !CHAIN) {
+  if constexpr (FAITH && !LITERAL && !CHAIN) {
     if (res) {  // MGX_FLAG_RESIDENT: the one-workgroup server of one-frame requests
       hipLaunchKernelGGL((extract_kernel<N, FAITH, LITERAL, SUB, LIGHT, NOTIME, CHAIN, false, true>), dim3(1), dim3(kThreads), lds,
                          stream, a);
       return hipGetLastError();
     }
+  }
+  if constexpr (N <= kInlineMaxN && FAITH && !LITERAL && !CHAIN) {
     if (inl) {  // the one frame in the kernel arguments (KernelArgsInline<N>)
       KernelArgsInline<N> x;
       x.a = a;
@@ -2694,14 +2696,14 @@ int extract_blocks_per_cu(int n, int precision, int mode, int ncoef, int nfilt, 
 hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, int grid,
                           hipStream_t stream, const float* inline_frame, bool resident) {
   if (a.num_frames != 1) inline_frame = nullptr;
-  if (resident && (a.num_frames != 1 || grid != 1 || n > kInlineMaxN || a.res_mail == nullptr || a.res_exit == nullptr ||
+  if (resident && (a.num_frames != 1 || grid != 1 || a.res_mail == nullptr || a.res_exit == nullptr ||
                    a.done_flag == nullptr))
     return hipErrorInvalidValue;
   switch (n) {
     case 256: return launch_prec<256>(precision, mode, a, grid, stream, inline_frame, resident);
     case 512: return launch_prec<512>(precision, mode, a, grid, stream, inline_frame, resident);
     case 1024: return launch_prec<1024>(precision, mode, a, grid, stream, inline_frame, resident);
-    case 2048: return launch_prec<2048>(precision, mode, a, grid, stream, nullptr, false);
+    case 2048: return launch_prec<2048>(precision, mode, a, grid, stream, nullptr, resident);
     default: return hipErrorInvalidValue;
   }
 }

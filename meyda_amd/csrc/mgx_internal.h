@@ -138,7 +138,7 @@ int hip_fail(hipError_t e, const char* what);
 // inline_frame (host memory, N floats): a one-frame launch at N <= kInlineMaxN passes its frame in the
 // kernel arguments (KernelArgsInline) when a faithful per-buffer kernel without the reference-order
 // chains runs it; a.frames is then not read. Otherwise ignored.
-// resident (MGX_FLAG_RESIDENT, one frame, grid 1, N <= kInlineMaxN, a.res_* set): the launch stays on the
+// resident (MGX_FLAG_RESIDENT, one frame, grid 1, a.res_* set): the launch stays on the
 // device serving requests from a.res_mail until the stop word or the idle timeout (kernels.hip res_wait);
 // the literal, fast and reference-order plans have no resident form (an error).
 hipError_t launch_extract(int n, int precision, int mode, const KernelArgs& a, int grid,

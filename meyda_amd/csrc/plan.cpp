@@ -636,10 +636,8 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   const bool pair = chain && nf <= mgx::kChainPairMaxMel;
   if (chain) chain_schedule(bins.data(), nf, L, pair ? 8 : 4, cs);
 
-  if ((d->flags & MGX_FLAG_RESIDENT) && (n > mgx::kInlineMaxN || d->precision != MGX_PRECISION_FAITHFUL ||
-                                         d->mode != MGX_MODE_PER_BUFFER_FFT || chain))
-    return fail(MGX_E_UNSUPPORTED, "MGX_FLAG_RESIDENT: faithful per-buffer plans of N <= %d without MGX_FLAG_MFCC_REFERENCE only",
-                mgx::kInlineMaxN);
+  if ((d->flags & MGX_FLAG_RESIDENT) && (d->precision != MGX_PRECISION_FAITHFUL || d->mode != MGX_MODE_PER_BUFFER_FFT || chain))
+    return fail(MGX_E_UNSUPPORTED, "MGX_FLAG_RESIDENT: faithful per-buffer plans without MGX_FLAG_MFCC_REFERENCE only");
 
   auto* p = new mgx_plan();
   p->d = *d;

@@ -135,7 +135,7 @@ class Meyda {
       mfccReferenceOrder: this.options.mfccReferenceOrder ? 1 : 0,
       // options.resident: one-buffer calls (the per-buffer process()/get() path) served by a workgroup that
       // stays on the device between buffers instead of one launch per buffer (include/meyda_gpu.h
-      // MGX_FLAG_RESIDENT); one device, faithful per-buffer plans of bufferSize <= 1024
+      // MGX_FLAG_RESIDENT); one device, faithful per-buffer plans without mfccReferenceOrder
       resident: this.options.resident && !Array.isArray(this.options.devices) ? 1 : 0,
       // options.devices = [d0, d1, ...]: every batch is sharded over the devices and the
       // per-frame features are gathered to d0 over xGMI (RCCL), include/meyda_gpu.h mgx_group_*

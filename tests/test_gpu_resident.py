@@ -52,7 +52,7 @@ def same(a, b, what):
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (what, k, x, y)
 
 
-@pytest.mark.parametrize("n", [256, 512, 1024])
+@pytest.mark.parametrize("n", [256, 512, 1024, 2048])
 def test_resident_matches_launch_per_call(capi, n):
     x = frames(n, 24)
     ref = capi.Plan(buffer_size=n, scalar_f64=True)
@@ -138,7 +138,7 @@ def test_resident_destroy_while_waiting(capi):
         assert time.perf_counter() - t0 < 0.5
 
 
-@pytest.mark.parametrize("kw", [dict(buffer_size=2048), dict(buffer_size=512, precision="fast"),
+@pytest.mark.parametrize("kw", [dict(buffer_size=512, precision="fast"),
                                 dict(buffer_size=512, mode="literal"), dict(buffer_size=512, mfcc_reference=True)])
 def test_resident_unsupported_plans(capi, kw):
     with pytest.raises(capi.MgxError):

@@ -38,7 +38,7 @@ def run(p, x, feats, calls):
 
 def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 3000
-    for n in (512, 1024):
+    for n in (512, 1024, 2048):
         x = np.random.default_rng(1).uniform(-1, 1, (1, n)).astype(np.float32)
         res = capi.Plan(buffer_size=n, scalar_f64=True, resident=True)
         lau = capi.Plan(buffer_size=n, scalar_f64=True)
