@@ -6,7 +6,7 @@
 // and the frame is complete when every tag is the request's (no ordering between words is assumed).
 //   A  the wave reads the whole mailbox every poll;
 //   B  it polls the first word only, then reads the whole mailbox (one more PCIe round trip);
-//   P  as A with two polls in flight;
+//   P  as A with two polls in flight; W as P, the answer written through without the system-scope release;
 //   L  a one-wave kernel launch per call that reads the same mailbox and answers the same way (the product's
 //      protocol today, minus its extraction).
 // The answer: the frame's sum (lane partial sums, DPP-free shuffles) in one host word, then the request number.
@@ -108,7 +108,17 @@ __device__ __forceinline__ bool check(const uint64_t (&w)[W], uint32_t seq, floa
   sum = s;
   return __all(bad == 0);
 }
-template <int W>
+// the answer without the system-scope release (no L2 write-back): both words written through (system-scope
+// relaxed stores), the second after the first's acknowledgement (s_waitcnt vmcnt(0))
+__device__ __forceinline__ void answer_wt(uint32_t* out, float sum, uint32_t seq) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(out + 1, __float_as_uint(sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_s_waitcnt(0);
+    __hip_atomic_store(out, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <int W, bool WT = false>
 __global__ void server_pipe(const uint64_t* mail, uint32_t* out, const uint32_t* stop, uint32_t* polls) {
   uint32_t seq = 1, npoll = 0;
   unsigned long long last = wall_clock64();
@@ -119,13 +129,15 @@ __global__ void server_pipe(const uint64_t* mail, uint32_t* out, const uint32_t*
     float sum;
     issue<W>(b, mail);
     if (check<W>(a, seq, sum)) {
-      answer(out, sum, seq);
+      if (WT) answer_wt(out, sum, seq);
+      else answer(out, sum, seq);
       ++seq;
       last = wall_clock64();
     }
     issue<W>(a, mail);
     if (check<W>(b, seq, sum)) {
-      answer(out, sum, seq);
+      if (WT) answer_wt(out, sum, seq);
+      else answer(out, sum, seq);
       ++seq;
       last = wall_clock64();
     }
@@ -183,7 +195,7 @@ int main(int argc, char** argv) {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   printf("{\"n\": %d, \"calls\": %d, ", n, calls);
-  for (int mode = 0; mode < 4; ++mode) {
+  for (int mode = 0; mode < 5; ++mode) {
     memset(hmail, 0, n * 8);
     *vout = 0;
     *vstop = 0;
@@ -191,6 +203,9 @@ int main(int argc, char** argv) {
     if (mode == 3) {
       if (n == 512) server_pipe<8><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
       else server_pipe<16><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
+    } else if (mode == 4) {
+      if (n == 512) server_pipe<8, true><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
+      else server_pipe<16, true><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
     } else if (mode < 2) {
       if (n == 512) {
         if (mode == 0) server<8, false><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
@@ -220,7 +235,8 @@ int main(int argc, char** argv) {
     }
     *vstop = 1;
     CK(hipStreamSynchronize(s));
-    report(mode == 0 ? "resident_full_poll" : mode == 1 ? "resident_head_poll" : mode == 2 ? "launch_per_call" : "resident_pipelined_poll", t);
+    report(mode == 0 ? "resident_full_poll" : mode == 1 ? "resident_head_poll" : mode == 2 ? "launch_per_call"
+           : mode == 3 ? "resident_pipelined_poll" : "resident_pipelined_poll_write_through", t);
   }
   printf("\"post_only_us\": ");
   {
