@@ -133,7 +133,9 @@ typedef struct mgx_plan_desc {
                                         mailbox over PCIe (about N x 16 bytes per microsecond) while it waits,
                                         and ends itself 20 ms after its last call (MGX_RESIDENT_IDLE_MS), on
                                         the plan's next call of any other kind, or at mgx_plan_destroy. A device
-                                        synchronisation made meanwhile waits for that end. Faithful per-buffer
+                                        synchronisation made meanwhile waits for that end. mgx_plan_create
+                                        pays the path's one-time set-up (~13 ms: pinned buffers, a hardware
+                                        queue, one warm-up call), not the first real-time call. Faithful per-buffer
                                         plans without MGX_FLAG_MFCC_REFERENCE only (MGX_E_UNSUPPORTED
                                         otherwise). */
 
