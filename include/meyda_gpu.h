@@ -130,7 +130,9 @@ typedef struct mgx_plan_desc {
                                         mgx_extract_host calls are served by one workgroup that stays on the
                                         device between calls, polling a mailbox in pinned host memory, instead
                                         of one launch per call. It holds one CU slot and reads the
-                                        mailbox over PCIe (about N x 16 bytes per microsecond) while it waits,
+                                        mailbox over PCIe (about N x 16 bytes per microsecond; with
+                                        MGX_RESIDENT_POLL=light its first word only, ~1 us more per call)
+                                        while it waits,
                                         and ends itself 20 ms after its last call (MGX_RESIDENT_IDLE_MS), on
                                         the plan's next call of any other kind, or at mgx_plan_destroy. A device
                                         synchronisation made meanwhile waits for that end. mgx_plan_create

@@ -1984,10 +1984,32 @@ __device__ __forceinline__ int res_take(const uint64_t (&w)[CH], uint32_t seq, f
 }
 // The wait for request seq: true with its frame in x; false on the stop word, or when res_idle ticks of the
 // 100 MHz clock pass without it (every launch ends on its own: a host that stops posting leaves no wave
-// behind for longer than the idle timeout).
+// behind for longer than the idle timeout). light (MGX_RESIDENT_POLL=light): the waiting reads only the first
+// word (8 bytes per read, two in flight, instead of the whole frame), then the frame is read until it is
+// whole -- one PCIe round trip more per request, for almost no PCIe traffic while waiting.
 template <int CH>
-__device__ __forceinline__ bool res_wait(const uint64_t* mail, uint32_t seq, uint32_t idle, float (&x)[CH], unsigned lane) {
+__device__ __forceinline__ bool res_wait(const uint64_t* mail, uint32_t seq, uint32_t idle, bool light, float (&x)[CH],
+                                         unsigned lane) {
   const unsigned long long t0 = wall_clock64();
+  if (light) {
+    const auto head = gbl(mail);
+    uint64_t h = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (;;) {
+      const uint64_t hn = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t tag = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(h >> 32));
+      if (tag == kResStop) return false;
+      if (tag == seq) break;
+      h = hn;
+      if (wall_clock64() - t0 > idle) return false;
+    }
+    for (;;) {  // (the host writes the frame in ~0.5 us: a read or two sees it whole)
+      uint64_t a[CH];
+      res_issue<CH>(a, mail, lane);
+      const int r = res_take<CH>(a, seq, x);
+      if (r != 0) return r > 0;
+      if (wall_clock64() - t0 > idle) return false;
+    }
+  }
   uint64_t a[CH], b[CH];
   res_issue<CH>(a, mail, lane);
   for (;;) {
@@ -2249,7 +2271,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RES ? 
     if constexpr (RES) {
       // the resident launch (one frame per request, wave 0; the others have no batch): the next request
       KArgs* q = args_ptr();
-      if (!res_wait<CH>(q->res_mail, rseq, q->res_idle, xr, (unsigned)lane)) break;
+      if (!res_wait<CH>(q->res_mail, rseq, q->res_idle, q->res_light != 0, xr, (unsigned)lane)) break;
       MGX_STAMP(0);  // (the diagnostic build: the request's stamps count from here)
       MGX_CLOCK_STAMP(13);
     }

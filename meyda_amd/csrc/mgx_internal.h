@@ -112,6 +112,7 @@ struct KernelArgs {
   uint32_t* res_exit;
   uint32_t res_seq;      // the first request number the launch serves
   uint32_t res_idle;     // idle timeout, ticks of the 100 MHz real-time clock
+  uint32_t res_light;    // poll the mailbox's first word only, then read the frame (MGX_RESIDENT_POLL=light)
 };
 constexpr uint32_t kResStop = 0xFFFFFFFFu;  // a request number that stops the resident launch
 

@@ -506,6 +506,7 @@ struct mgx_plan {
   // MGX_FLAG_RESIDENT: one-frame host calls served by a launch that stays on the device (resident_request)
   bool resident = false;
   uint32_t res_idle_ms = 20;   // its idle timeout (MGX_RESIDENT_IDLE_MS overrides)
+  bool res_light = false;      // MGX_RESIDENT_POLL=light: the launch polls the first word only (kernels.hip res_wait)
   hipStream_t s_res = nullptr; // its own stream: nothing else is queued behind it
   uint64_t* h_mail = nullptr;  // pinned, mapped: N request words (KernelArgs::res_mail), then the exit word
   uint64_t* d_mail = nullptr;  // the device address of h_mail
@@ -666,6 +667,7 @@ int mgx_plan_create(const mgx_plan_desc* d, mgx_plan** out) {
   if (const char* pp = getenv("MGX_POOL_PCT")) p->pool_pct = std::min(50, std::max(0, atoi(pp)));
   if (const char* nm = getenv("MGX_NT_MIN_MB")) p->nt_min_bytes = (uint64_t)std::max(0, atoi(nm)) << 20;
   if (const char* ri = getenv("MGX_RESIDENT_IDLE_MS")) p->res_idle_ms = (uint32_t)std::min(10000, std::max(1, atoi(ri)));
+  if (const char* rp = getenv("MGX_RESIDENT_POLL")) p->res_light = strcmp(rp, "light") == 0;
 
   size_t off = 0;
   const size_t o_win = carve<float>(off, n), o_tw = carve<double>(off, tw.size()),
@@ -917,6 +919,7 @@ int extract_device_impl(mgx_plan* p, const float* frames, uint64_t nframes, cons
     a.res_exit = reinterpret_cast<uint32_t*>(p->d_mail + p->n);
     a.res_seq = res->seq;
     a.res_idle = p->res_idle_ms * 100000u;  // the 100 MHz real-time clock
+    a.res_light = p->res_light ? 1 : 0;
     a.done_flag = const_cast<uint32_t*>(done);
     e = mgx::launch_extract(p->n, (int)p->d.precision, (int)p->d.mode, a, 1, (hipStream_t)stream, nullptr, true);
     return e == hipSuccess ? MGX_OK : hip_fail(e, "resident launch");

@@ -262,3 +262,26 @@ def test_resident_process_exit_with_a_live_launch(capi, how):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr[-2000:]
     assert time.perf_counter() - t0 < 30
+
+
+@pytest.mark.parametrize("n", [512, 2048])
+def test_resident_light_poll(capi, n):
+    # MGX_RESIDENT_POLL=light: the waiting launch reads the mailbox's first word only, then the frame
+    x = frames(n, 12, seed=12)
+    old = os.environ.get("MGX_RESIDENT_POLL")
+    os.environ["MGX_RESIDENT_POLL"] = "light"
+    try:
+        res = capi.Plan(buffer_size=n, scalar_f64=True, resident=True)
+    finally:
+        if old is None:
+            del os.environ["MGX_RESIDENT_POLL"]
+        else:
+            os.environ["MGX_RESIDENT_POLL"] = old
+    ref = capi.Plan(buffer_size=n, scalar_f64=True)
+    try:
+        for feats in (["rms", "spectralCentroid"], ALL, ["amplitudeSpectrum", "zcr"]):
+            for i in range(x.shape[0]):
+                same(res.extract(x[i:i + 1], feats), ref.extract(x[i:i + 1], feats), (n, feats, i))
+    finally:
+        res.close()
+        ref.close()

@@ -2,7 +2,7 @@
 """Where a resident one-frame call's time goes (MGX_FLAG_RESIDENT): the median time of
 mgx_extract_host on one frame per feature set, resident and launched per call, through the C ABI
 (ctypes: its own overhead is the same in every row). Time-domain sets skip the FFT; the differences
-between rows are the cost of the parts each set adds.
+between rows are the cost of the parts each set adds. resident_light: MGX_RESIDENT_POLL=light.
 usage: resident_features.py [calls]"""
 import ctypes
 import json
@@ -41,12 +41,17 @@ def main():
     for n in (512, 1024, 2048):
         x = np.random.default_rng(1).uniform(-1, 1, (1, n)).astype(np.float32)
         res = capi.Plan(buffer_size=n, scalar_f64=True, resident=True)
+        os.environ["MGX_RESIDENT_POLL"] = "light"
+        light = capi.Plan(buffer_size=n, scalar_f64=True, resident=True)
+        del os.environ["MGX_RESIDENT_POLL"]
         lau = capi.Plan(buffer_size=n, scalar_f64=True)
         for feats in SETS:
             r = {"n": n, "features": feats if len(feats) < 5 else "all (%d)" % len(feats),
-                 "resident_us": run(res, x, feats, calls), "launched_us": run(lau, x, feats, calls)}
+                 "resident_us": run(res, x, feats, calls), "resident_light_us": run(light, x, feats, calls),
+                 "launched_us": run(lau, x, feats, calls)}
             print(json.dumps(r), flush=True)
         res.close()
+        light.close()
         lau.close()
 
 
