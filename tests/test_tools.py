@@ -39,3 +39,16 @@ def test_gather_trace_splits_a_call_into_its_waits(tmp_path, capsys):
     gt.report({r: [c for c in cs if c[0][3] == 1024] for r, cs in calls.items()}, 20)
     out = capsys.readouterr().out
     assert "rank 0 (root)" in out and "rank 1 (peer)" in out and "post -> root's copy issued: median 5.0 us" in out
+
+
+def test_reference_order_log_emulation_is_exact(tmp_path):
+    # tools/emu/ref_ln_check.c: the reference-order MFCC's fast log (kernels.hip ref_ln: plan table, degree-6
+    # polynomial, interval check, library fallback) against glibc's double log rounded to float32 on 23.5 M
+    # floats -- the claim that lets the fast path replace the library log bit for bit
+    import subprocess
+    exe = str(tmp_path / "ref_ln_check")
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", os.path.join(ROOT, "tools", "emu", "ref_ln_check.c"), "-lm",
+                           "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120).stdout
+    assert "checked 23538910 floats: 0 mismatches" in out, out[-2000:]
+    assert "err " not in out, out[-2000:]  # the |y - ln x| bound held everywhere
