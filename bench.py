@@ -252,6 +252,9 @@ def latency_js():
     out = json.loads(r.stdout.strip().splitlines()[-1])
     out["status"] = "ok"
     out["env"] = {"HIP_FORCE_DEV_KERNARG": env["HIP_FORCE_DEV_KERNARG"]}
+    out["note"] = ("c1: a launch per get() (the facade's default); c1_resident: options.resident -- one workgroup stays on "
+                   "the device and takes each buffer from a pinned mailbox (MGX_FLAG_RESIDENT, DESIGN.md 9.1); *_gap: the "
+                   "host idle 1 ms between calls, as between a real-time source's buffers; medians in us per call")
     return out
 
 
