@@ -209,7 +209,7 @@ def test_resident_launch_leaves_other_launches_their_speed(capi):
     big = capi.Plan(buffer_size=n)
     out, o = big.alloc_outputs(F, ALL)
 
-    def launch_ms(reps=5):
+    def launch_ms(reps=9):
         s = torch.cuda.current_stream()
         big.extract_device(xd.data_ptr(), F, o, s.cuda_stream)  # (warm)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -241,7 +241,7 @@ def test_resident_launch_leaves_other_launches_their_speed(capi):
         res.close()
         big.close()
     print("launch alone %.4f ms, beside a resident launch %.4f ms" % (alone, beside))
-    assert beside < 1.25 * alone, (alone, beside)
+    assert beside < 1.3 * alone, (alone, beside)  # (measured +5 %; a slot left waiting would be ~2x)
 
 
 @pytest.mark.parametrize("how", ["exit", "os._exit"])
