@@ -7,6 +7,7 @@
 //   A  the wave reads the whole mailbox every poll;
 //   B  it polls the first word only, then reads the whole mailbox (one more PCIe round trip);
 //   P  as A with two polls in flight; W as P, the answer written through without the system-scope release;
+//   Q  as A with four polls in flight;
 //   L  a one-wave kernel launch per call that reads the same mailbox and answers the same way (the product's
 //      protocol today, minus its extraction).
 // The answer: the frame's sum (lane partial sums, DPP-free shuffles) in one host word, then the request number.
@@ -148,6 +149,32 @@ __global__ void server_pipe(const uint64_t* mail, uint32_t* out, const uint32_t*
   if (threadIdx.x == 0) polls[0] = npoll;
 }
 
+// Q: four reads in flight (a round trip's worth of reads issued at a quarter of it apart)
+template <int W>
+__global__ void server_pipe4(const uint64_t* mail, uint32_t* out, const uint32_t* stop, uint32_t* polls) {
+  uint32_t seq = 1;
+  unsigned long long last = wall_clock64();
+  const unsigned long long limit = 200000000ull;
+  uint64_t a[W], b[W], c[W], d[W];
+  issue<W>(a, mail);
+  issue<W>(b, mail);
+  issue<W>(c, mail);
+  for (;;) {
+    float sum;
+    issue<W>(d, mail);
+    if (check<W>(a, seq, sum)) { answer(out, sum, seq); ++seq; last = wall_clock64(); }
+    issue<W>(a, mail);
+    if (check<W>(b, seq, sum)) { answer(out, sum, seq); ++seq; last = wall_clock64(); }
+    issue<W>(b, mail);
+    if (check<W>(c, seq, sum)) { answer(out, sum, seq); ++seq; last = wall_clock64(); }
+    issue<W>(c, mail);
+    if (check<W>(d, seq, sum)) { answer(out, sum, seq); ++seq; last = wall_clock64(); }
+    if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
+    if (wall_clock64() - last > limit) break;
+  }
+  if (threadIdx.x == 0) polls[0] = seq;
+}
+
 template <int W>
 __global__ void one_shot(const uint64_t* mail, uint32_t* out, uint32_t seq) {
   float sum = 0.0f;
@@ -195,7 +222,7 @@ int main(int argc, char** argv) {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   printf("{\"n\": %d, \"calls\": %d, ", n, calls);
-  for (int mode = 0; mode < 5; ++mode) {
+  for (int mode = 0; mode < 6; ++mode) {
     memset(hmail, 0, n * 8);
     *vout = 0;
     *vstop = 0;
@@ -203,6 +230,9 @@ int main(int argc, char** argv) {
     if (mode == 3) {
       if (n == 512) server_pipe<8><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
       else server_pipe<16><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
+    } else if (mode == 5) {
+      if (n == 512) server_pipe4<8><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
+      else server_pipe4<16><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
     } else if (mode == 4) {
       if (n == 512) server_pipe<8, true><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
       else server_pipe<16, true><<<1, 64, 0, s>>>(dmail, dout, dstop, dpolls);
@@ -236,7 +266,8 @@ int main(int argc, char** argv) {
     *vstop = 1;
     CK(hipStreamSynchronize(s));
     report(mode == 0 ? "resident_full_poll" : mode == 1 ? "resident_head_poll" : mode == 2 ? "launch_per_call"
-           : mode == 3 ? "resident_pipelined_poll" : "resident_pipelined_poll_write_through", t);
+           : mode == 3 ? "resident_pipelined_poll" : mode == 4 ? "resident_pipelined_poll_write_through"
+           : "resident_four_reads_in_flight", t);
   }
   printf("\"post_only_us\": ");
   {
